@@ -1,0 +1,204 @@
+/*
+ * jwave_hip.h — C ABI of libjwave_hip.so, the MI355X (gfx950) engine for
+ * JWave's FWT / WPT / MODWT convolve-decimate hot path.
+ *
+ * This is the boundary a JNI shim (or ctypes / cgo / N-API) binds.  Plain C
+ * types only: pointers, sizes, ints.  Each entry point names the reference
+ * interface it replaces (paths under /root/reference/src/main/java/jwave/).
+ *
+ * Conventions
+ *  - Return value: JWV_OK (0) or an error code; the message (the reference's
+ *    exception text where one exists) is in jwv_last_error(ctx).
+ *  - Host-pointer entry points (no suffix) copy to the device, compute and copy
+ *    back; they return when the result is in `y`.
+ *  - `_dev` entry points take device pointers and are asynchronous on the
+ *    context's stream (jwv_ctx_set_stream); call jwv_ctx_synchronize or sync
+ *    the stream before reading results.  `y` must not overlap `x`.
+ *  - Inputs are never modified and pointers are not retained after return
+ *    (the reference never mutates inputs: FastWaveletTransform.java:85,
+ *    WaveletPacketTransform.java:86-88, MODWTTransform.java:288).
+ *  - Arrays are row-major and contiguous unless an `ld` is given.
+ *  - Thread safety: a context serialises its own calls with a mutex; use one
+ *    context per thread for concurrency (the reference transforms are
+ *    stateless and called concurrently: ParallelTransform.java:258-270).
+ */
+#ifndef JWAVE_HIP_H
+#define JWAVE_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define JWV_OK 0
+/* Invalid input that the reference reports with JWaveFailure (length not 2^p,
+ * level out of range): FastWaveletTransform.java:74-83,122-131,
+ * WaveletPacketTransform.java:76-84,144-152. */
+#define JWV_ERR_FAILURE 1
+/* MODWT level checks that the reference reports with IllegalArgumentException
+ * (MODWTTransform.java:257-282). */
+#define JWV_ERR_ILLEGAL_ARGUMENT 2
+/* Device / runtime failure (HIP error, out of memory): maps to JWaveError. */
+#define JWV_ERR_DEVICE 3
+/* Null pointer, bad tap table, overlapping buffers, size beyond int range. */
+#define JWV_ERR_BAD_CALL 4
+
+/* Math modes.  EXACT: a*b+c rounded twice, reference summation order — results
+ * are bit-identical to the JVM's.  FMA: fused multiply-add (one rounding) in
+ * the same order; differs from EXACT by ~1 ulp per tap. */
+#define JWV_MATH_EXACT 0
+#define JWV_MATH_FMA 1
+
+#define JWV_MAX_TAPS 64
+
+/* A filter bank, read once from the Wavelet getters
+ * (transforms/wavelets/Wavelet.java:152-219). */
+typedef struct jwv_taps {
+  int32_t mother_wavelength;    /* L = getMotherWavelength(), 2..64 */
+  int32_t transform_wavelength; /* getTransformWavelength(), normally 2 */
+  const double* lo;             /* getScalingDeComposition()   (L doubles) */
+  const double* hi;             /* getWaveletDeComposition()   (L doubles) */
+  const double* lo_r;           /* getScalingReConstruction()  (L doubles) */
+  const double* hi_r;           /* getWaveletReConstruction()  (L doubles) */
+  /* 1.0, or 0.5 for Haar1Orthogonal whose reverse() scales every synthesis
+   * term (transforms/wavelets/haar/Haar1Orthogonal.java:39,175-207). */
+  double reverse_scale;
+} jwv_taps;
+
+typedef struct jwv_ctx jwv_ctx;
+
+/* ---- context -------------------------------------------------------------- */
+int jwv_ctx_create(int device, jwv_ctx** out);
+int jwv_ctx_destroy(jwv_ctx* ctx);
+/* Last error message of this context ("" if none).  ctx may be NULL: then the
+ * calling thread's last context-less error (e.g. from jwv_ctx_create). */
+const char* jwv_last_error(const jwv_ctx* ctx);
+/* Use a caller-owned hipStream_t (NULL = the context's own stream). */
+int jwv_ctx_set_stream(jwv_ctx* ctx, void* hip_stream);
+void* jwv_ctx_get_stream(const jwv_ctx* ctx);
+int jwv_ctx_set_math(jwv_ctx* ctx, int mode);
+int jwv_ctx_synchronize(jwv_ctx* ctx);
+/* Profiling: when enabled, every kernel launch is bracketed by a pair of
+ * hipEvents recorded on the launch stream.  profile_read synchronises, sums the
+ * event times per kernel kind (fwt_fwd_tile, fwt_rev_res, ...), clears the
+ * records and fills up to max_out entries; *n_out = number of kinds seen.
+ * `bytes` is the algorithmic HBM traffic of those launches. */
+typedef struct jwv_kernel_stat {
+  char name[32];
+  int64_t launches;
+  double total_ms;
+  double bytes;
+} jwv_kernel_stat;
+int jwv_ctx_profile_enable(jwv_ctx* ctx, int on);
+int jwv_ctx_profile_read(jwv_ctx* ctx, jwv_kernel_stat* out, int max_out, int* n_out);
+/* Release cached device workspace. */
+int jwv_ctx_trim(jwv_ctx* ctx);
+int jwv_version(void);
+
+/* ---- 1-D FWT ---------------------------------------------------------------
+ * FastWaveletTransform.forward(double[], int level)  FastWaveletTransform.java:71-101
+ * FastWaveletTransform.reverse(double[], int level)  FastWaveletTransform.java:119-153
+ * (full depth, WaveletTransform.forward/reverse(double[]) :77-112, is
+ *  level = log2(n)). */
+int jwv_fwt_fwd_f64(const double* x, double* y, int64_t n, int level, const jwv_taps* t,
+                    jwv_ctx* ctx);
+int jwv_fwt_rev_f64(const double* y, double* x, int64_t n, int level, const jwv_taps* t,
+                    jwv_ctx* ctx);
+int jwv_fwt_fwd_f64_dev(const double* x, double* y, int64_t n, int level, const jwv_taps* t,
+                        jwv_ctx* ctx);
+int jwv_fwt_rev_f64_dev(const double* y, double* x, int64_t n, int level, const jwv_taps* t,
+                        jwv_ctx* ctx);
+
+/* Batched 1-D FWT: `batch` independent signals of length n, signal b at
+ * x + b*ld (ld >= n); the same for y.  Equivalent to one forward(double[],
+ * level) per signal (the batch loop of ParallelizationOpportunityTest.java:80-98). */
+int jwv_fwt_fwd_batch_f64(const double* x, double* y, int64_t batch, int64_t n, int64_t ld,
+                          int level, const jwv_taps* t, jwv_ctx* ctx);
+int jwv_fwt_rev_batch_f64(const double* y, double* x, int64_t batch, int64_t n, int64_t ld,
+                          int level, const jwv_taps* t, jwv_ctx* ctx);
+int jwv_fwt_fwd_batch_f64_dev(const double* x, double* y, int64_t batch, int64_t n, int64_t ld,
+                              int level, const jwv_taps* t, jwv_ctx* ctx);
+int jwv_fwt_rev_batch_f64_dev(const double* y, double* x, int64_t batch, int64_t n, int64_t ld,
+                              int level, const jwv_taps* t, jwv_ctx* ctx);
+
+/* ---- 2-D / 3-D FWT -----------------------------------------------------------
+ * BasicTransform.forward(double[][], lvlM, lvlN)  BasicTransform.java:361-399
+ *   (rows with lvlN, then columns with lvlM); reverse :436-474 (columns, then
+ *   rows).  x is rows*cols row-major (a JNI shim packs double[][] rows).
+ * BasicTransform.forward(double[][][], lvlP, lvlQ, lvlR)  :509-560 — slice
+ *   [i][.][.] gets the 2-D transform with (lvlP, lvlQ), then the lines along i
+ *   get lvlR; reverse :602-659.  x is P*Q*R row-major. */
+int jwv_fwt2d_fwd_f64(const double* x, double* y, int64_t rows, int64_t cols, int lvl_m,
+                      int lvl_n, const jwv_taps* t, jwv_ctx* ctx);
+int jwv_fwt2d_rev_f64(const double* y, double* x, int64_t rows, int64_t cols, int lvl_m,
+                      int lvl_n, const jwv_taps* t, jwv_ctx* ctx);
+int jwv_fwt2d_fwd_f64_dev(const double* x, double* y, int64_t rows, int64_t cols, int lvl_m,
+                          int lvl_n, const jwv_taps* t, jwv_ctx* ctx);
+int jwv_fwt2d_rev_f64_dev(const double* y, double* x, int64_t rows, int64_t cols, int lvl_m,
+                          int lvl_n, const jwv_taps* t, jwv_ctx* ctx);
+int jwv_fwt3d_fwd_f64(const double* x, double* y, int64_t p, int64_t q, int64_t r, int lvl_p,
+                      int lvl_q, int lvl_r, const jwv_taps* t, jwv_ctx* ctx);
+int jwv_fwt3d_rev_f64(const double* y, double* x, int64_t p, int64_t q, int64_t r, int lvl_p,
+                      int lvl_q, int lvl_r, const jwv_taps* t, jwv_ctx* ctx);
+int jwv_fwt3d_fwd_f64_dev(const double* x, double* y, int64_t p, int64_t q, int64_t r,
+                          int lvl_p, int lvl_q, int lvl_r, const jwv_taps* t, jwv_ctx* ctx);
+int jwv_fwt3d_rev_f64_dev(const double* y, double* x, int64_t p, int64_t q, int64_t r,
+                          int lvl_p, int lvl_q, int lvl_r, const jwv_taps* t, jwv_ctx* ctx);
+
+/* ---- WPT ---------------------------------------------------------------------
+ * WaveletPacketTransform.forward(double[], int level)  WaveletPacketTransform.java:73-124
+ * WaveletPacketTransform.reverse(double[], int level)  WaveletPacketTransform.java:141-191
+ * (same math: PooledWaveletPacketTransform, ParallelWaveletPacketTransform). */
+int jwv_wpt_fwd_f64(const double* x, double* y, int64_t n, int level, const jwv_taps* t,
+                    jwv_ctx* ctx);
+int jwv_wpt_rev_f64(const double* y, double* x, int64_t n, int level, const jwv_taps* t,
+                    jwv_ctx* ctx);
+int jwv_wpt_fwd_f64_dev(const double* x, double* y, int64_t n, int level, const jwv_taps* t,
+                        jwv_ctx* ctx);
+int jwv_wpt_rev_f64_dev(const double* y, double* x, int64_t n, int level, const jwv_taps* t,
+                        jwv_ctx* ctx);
+int jwv_wpt_fwd_batch_f64(const double* x, double* y, int64_t batch, int64_t n, int64_t ld,
+                          int level, const jwv_taps* t, jwv_ctx* ctx);
+int jwv_wpt_rev_batch_f64(const double* y, double* x, int64_t batch, int64_t n, int64_t ld,
+                          int level, const jwv_taps* t, jwv_ctx* ctx);
+int jwv_wpt_fwd_batch_f64_dev(const double* x, double* y, int64_t batch, int64_t n, int64_t ld,
+                              int level, const jwv_taps* t, jwv_ctx* ctx);
+int jwv_wpt_rev_batch_f64_dev(const double* y, double* x, int64_t batch, int64_t n, int64_t ld,
+                              int level, const jwv_taps* t, jwv_ctx* ctx);
+/* 2-D / 3-D packet transforms through the same BasicTransform loops. */
+int jwv_wpt2d_fwd_f64(const double* x, double* y, int64_t rows, int64_t cols, int lvl_m,
+                      int lvl_n, const jwv_taps* t, jwv_ctx* ctx);
+int jwv_wpt2d_rev_f64(const double* y, double* x, int64_t rows, int64_t cols, int lvl_m,
+                      int lvl_n, const jwv_taps* t, jwv_ctx* ctx);
+int jwv_wpt2d_fwd_f64_dev(const double* x, double* y, int64_t rows, int64_t cols, int lvl_m,
+                          int lvl_n, const jwv_taps* t, jwv_ctx* ctx);
+int jwv_wpt2d_rev_f64_dev(const double* y, double* x, int64_t rows, int64_t cols, int lvl_m,
+                          int lvl_n, const jwv_taps* t, jwv_ctx* ctx);
+int jwv_wpt3d_fwd_f64(const double* x, double* y, int64_t p, int64_t q, int64_t r, int lvl_p,
+                      int lvl_q, int lvl_r, const jwv_taps* t, jwv_ctx* ctx);
+int jwv_wpt3d_rev_f64(const double* y, double* x, int64_t p, int64_t q, int64_t r, int lvl_p,
+                      int lvl_q, int lvl_r, const jwv_taps* t, jwv_ctx* ctx);
+
+/* ---- MODWT -------------------------------------------------------------------
+ * MODWTTransform.forwardMODWT(double[] data, int maxLevel)  MODWTTransform.java:256-306
+ *   wv receives (J+1)*n doubles, row-major [W_1 .. W_J, V_J] (coeffs[0..J]).
+ *   DIRECT circular convolution semantics (:677-690).
+ * MODWTTransform.inverseMODWT(double[][] coefficients)     MODWTTransform.java:337-375
+ *   wv as produced by the forward; J = coefficients.length - 1. */
+int jwv_modwt_fwd_f64(const double* x, double* wv, int64_t n, int J, const jwv_taps* t,
+                      jwv_ctx* ctx);
+int jwv_modwt_inv_f64(const double* wv, double* x, int64_t n, int J, const jwv_taps* t,
+                      jwv_ctx* ctx);
+int jwv_modwt_fwd_f64_dev(const double* x, double* wv, int64_t n, int J, const jwv_taps* t,
+                          jwv_ctx* ctx);
+int jwv_modwt_inv_f64_dev(const double* wv, double* x, int64_t n, int J, const jwv_taps* t,
+                          jwv_ctx* ctx);
+/* The MODWT filters g, h (L doubles each) the engine derives from t
+ * (MODWTTransform.initializeFilterCache :452-484). Host-only, no device. */
+int jwv_modwt_filters(const jwv_taps* t, double* g, double* h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* JWAVE_HIP_H */

@@ -1,0 +1,144 @@
+"""ctypes binding of libjwave_hip.so (the C ABI declared in include/jwave_hip.h).
+
+The library is the only compute path: there is no CPU fallback.  If the
+shared object is missing or fails to load, ``lib()`` raises ``JWaveError``.
+"""
+import ctypes
+import os
+import re
+import threading
+
+from .exceptions import JWaveError
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libjwave_hip.so")
+HEADER = os.path.join(HERE, "..", "include", "jwave_hip.h")
+
+JWV_OK = 0
+JWV_ERR_FAILURE = 1
+JWV_ERR_ILLEGAL_ARGUMENT = 2
+JWV_ERR_DEVICE = 3
+JWV_ERR_BAD_CALL = 4
+JWV_MATH_EXACT = 0
+JWV_MATH_FMA = 1
+
+_dp = ctypes.c_void_p  # device or host double*
+_i64 = ctypes.c_int64
+_int = ctypes.c_int
+
+
+class Taps(ctypes.Structure):
+    _fields_ = [("mother_wavelength", ctypes.c_int32),
+                ("transform_wavelength", ctypes.c_int32),
+                ("lo", ctypes.POINTER(ctypes.c_double)),
+                ("hi", ctypes.POINTER(ctypes.c_double)),
+                ("lo_r", ctypes.POINTER(ctypes.c_double)),
+                ("hi_r", ctypes.POINTER(ctypes.c_double)),
+                ("reverse_scale", ctypes.c_double)]
+
+
+_TP = ctypes.POINTER(Taps)
+
+
+class KernelStat(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 32), ("launches", ctypes.c_int64),
+                ("total_ms", ctypes.c_double), ("bytes", ctypes.c_double)]
+
+_CTX = ctypes.c_void_p
+
+# name -> argtypes (restype int unless listed in _RESTYPES)
+_SIGS = {
+    "jwv_version": [],
+    "jwv_ctx_create": [_int, ctypes.POINTER(ctypes.c_void_p)],
+    "jwv_ctx_destroy": [_CTX],
+    "jwv_last_error": [_CTX],
+    "jwv_ctx_set_stream": [_CTX, ctypes.c_void_p],
+    "jwv_ctx_get_stream": [_CTX],
+    "jwv_ctx_set_math": [_CTX, _int],
+    "jwv_ctx_synchronize": [_CTX],
+    "jwv_ctx_trim": [_CTX],
+    "jwv_ctx_profile_enable": [_CTX, _int],
+    "jwv_ctx_profile_read": [_CTX, ctypes.POINTER(KernelStat), _int, ctypes.POINTER(_int)],
+    "jwv_modwt_filters": [_TP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)],
+}
+for _n in ("fwt_fwd", "fwt_rev", "wpt_fwd", "wpt_rev"):
+    for _s in ("", "_dev"):
+        _SIGS["jwv_%s_f64%s" % (_n, _s)] = [_dp, _dp, _i64, _int, _TP, _CTX]
+        _SIGS["jwv_%s_batch_f64%s" % (_n, _s)] = [_dp, _dp, _i64, _i64, _i64, _int, _TP, _CTX]
+for _n in ("fwt2d_fwd", "fwt2d_rev"):
+    for _s in ("", "_dev"):
+        _SIGS["jwv_%s_f64%s" % (_n, _s)] = [_dp, _dp, _i64, _i64, _int, _int, _TP, _CTX]
+for _n in ("wpt2d_fwd", "wpt2d_rev"):
+    for _s in ("", "_dev"):
+        _SIGS["jwv_%s_f64%s" % (_n, _s)] = [_dp, _dp, _i64, _i64, _int, _int, _TP, _CTX]
+for _n in ("fwt3d_fwd", "fwt3d_rev"):
+    for _s in ("", "_dev"):
+        _SIGS["jwv_%s_f64%s" % (_n, _s)] = [_dp, _dp, _i64, _i64, _i64, _int, _int, _int, _TP, _CTX]
+for _n in ("wpt3d_fwd", "wpt3d_rev"):
+    _SIGS["jwv_%s_f64" % _n] = [_dp, _dp, _i64, _i64, _i64, _int, _int, _int, _TP, _CTX]
+for _n in ("modwt_fwd", "modwt_inv"):
+    for _s in ("", "_dev"):
+        _SIGS["jwv_%s_f64%s" % (_n, _s)] = [_dp, _dp, _i64, _int, _TP, _CTX]
+
+_RESTYPES = {"jwv_last_error": ctypes.c_char_p, "jwv_ctx_get_stream": ctypes.c_void_p}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def hip_runtimes_mapped():
+    """Paths of libamdhip64 copies mapped into this process (expect exactly one)."""
+    out = set()
+    try:
+        with open("/proc/self/maps") as fh:
+            for line in fh:
+                if "libamdhip64" in line:
+                    out.add(line.split()[-1])
+    except OSError:
+        pass
+    return sorted(out)
+
+
+def header_symbols():
+    """Function names declared in include/jwave_hip.h."""
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", " ", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(jwv_[a-z0-9_]+)\s*\(", txt)))
+
+
+def lib(path=None):
+    """Load libjwave_hip.so (building it first if the sources are newer)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        p = path or LIB_PATH
+        # One HIP runtime per process: torch bundles its own libamdhip64.so
+        # (SONAME libamdhip64.so.7, the same SONAME as /opt/rocm's).  If torch
+        # is loaded first, the dynamic linker binds our NEEDED entry to torch's
+        # copy; loaded the other way round, two runtimes would fight over the
+        # device ("No HIP GPUs are available" in torch).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        if os.environ.get("JWAVE_AMD_NO_BUILD") != "1":
+            try:
+                from . import _build
+                if _build.stale():
+                    _build.build()
+            except Exception as e:  # build tools missing: fall through to load
+                if not os.path.exists(p):
+                    raise JWaveError("libjwave_hip.so missing and build failed: %s" % e)
+        if not os.path.exists(p):
+            raise JWaveError("libjwave_hip.so not found at %s (run __graft_entry__.build())" % p)
+        try:
+            L = ctypes.CDLL(p)
+        except OSError as e:
+            raise JWaveError("cannot load %s: %s" % (p, e))
+        for name, args in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = _RESTYPES.get(name, ctypes.c_int)
+        _lib = L
+        return _lib

@@ -1,0 +1,974 @@
+// capi.cpp — C ABI of libjwave_hip.so: validation (reference messages), the
+// pass planner, device workspace and host<->device staging.
+//
+// Every FWT / WPT transform is an "axis transform" over a [outer][len][inner]
+// block (see jwv_device.hpp); the planner splits the reference's level loop
+// into device passes:
+//   forward : tiled passes of K fused levels while the level input is longer
+//             than one block's LDS can hold, then one resident pass for the
+//             rest (FastWaveletTransform.java:90-97, WaveletPacketTransform.java:95-121);
+//   reverse : a resident pass for the small levels, then tiled passes
+//             (FastWaveletTransform.java:137-149, WaveletPacketTransform.java:163-188).
+// 2-D / 3-D transforms are sequences of axis transforms in the order of
+// BasicTransform.java:361-474 / 509-659.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/jwave_hip.h"
+#include "jwv_launch.hpp"
+
+using jwv::AxisView;
+using jwv::Bank;
+using jwv::Geo;
+
+namespace {
+
+thread_local std::string g_tls_error;
+
+struct DevBuf {
+  double* p = nullptr;
+  size_t n = 0;  // doubles
+};
+
+}  // namespace
+
+struct jwv_ctx {
+  int device = 0;
+  hipStream_t own = nullptr;
+  hipStream_t stream = nullptr;
+  int math = JWV_MATH_EXACT;
+  std::string err;
+  std::mutex mu;
+  DevBuf ws[2];  // small ping-pong scratch (level approximations)
+  DevBuf big;    // full-size intermediate between 2-D/3-D axes
+  DevBuf big2;   // full-size intermediate between multi-pass WPT passes
+  DevBuf hin, hout;  // staging for the host-pointer entry points
+  // profiling: hipEvent pairs around every kernel launch on the launch stream
+  bool prof = false;
+  struct Rec { int kind; double bytes; hipEvent_t e0, e1; };
+  std::vector<Rec> recs;
+  std::vector<hipEvent_t> ev_pool;
+};
+
+namespace {
+
+struct Fail {
+  int code;
+  std::string msg;
+};
+
+int set_err(jwv_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg; else g_tls_error = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                \
+  do {                                                                              \
+    hipError_t e_ = (expr);                                                         \
+    if (e_ != hipSuccess)                                                           \
+      throw Fail{JWV_ERR_DEVICE, std::string("HIP error: ") + hipGetErrorString(e_) + \
+                                     " at " #expr};                                 \
+  } while (0)
+
+// MathToolKit.isBinary — tools/MathToolKit.java:185-188
+bool is_binary(int64_t n) { return n > 0 && (n & (n - 1)) == 0; }
+// BasicTransform.calcExponent / MathToolKit.getExponent (:202-206) — exact
+// for powers of two in int range.
+int exponent(int64_t n) {
+  int e = 0;
+  while ((int64_t(1) << (e + 1)) <= n) ++e;
+  return e;
+}
+
+Bank make_bank(const jwv_taps* t) {
+  if (!t) throw Fail{JWV_ERR_BAD_CALL, "jwv_taps is NULL"};
+  if (t->mother_wavelength < 1 || t->mother_wavelength > JWV_MAX_TAPS)
+    throw Fail{JWV_ERR_BAD_CALL, "mother_wavelength must be in [1, 64]"};
+  if (t->transform_wavelength < 1)
+    throw Fail{JWV_ERR_BAD_CALL, "transform_wavelength must be >= 1"};
+  if (!t->lo || !t->hi || !t->lo_r || !t->hi_r)
+    throw Fail{JWV_ERR_BAD_CALL, "tap pointer is NULL"};
+  Bank b;
+  b.L = t->mother_wavelength;
+  b.tw = t->transform_wavelength;
+  for (int j = 0; j < b.L; ++j) {
+    b.lo[j] = t->lo[j]; b.hi[j] = t->hi[j]; b.lo_r[j] = t->lo_r[j]; b.hi_r[j] = t->hi_r[j];
+  }
+  b.scale = t->reverse_scale;
+  return b;
+}
+
+AxisView cview(int64_t len, int64_t inner) {
+  AxisView v{};
+  v.s_outer = len * inner;
+  v.s_pk = 0;
+  v.s_len = inner;
+  v.pk = 1;
+  return v;
+}
+
+AxisView with_packets(AxisView v, int pk, int h) {
+  v.pk = pk;
+  v.s_pk = (int64_t)h * v.s_len;
+  return v;
+}
+
+// grow-only device buffer; synchronises the stream before freeing (a queued
+// kernel may still use the old buffer).
+double* grow(jwv_ctx* c, DevBuf& b, size_t n) {
+  if (b.n >= n) return b.p;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (b.p) HIPCHK(hipFree(b.p));
+  b.p = nullptr;
+  b.n = 0;
+  HIPCHK(hipMalloc(&b.p, std::max<size_t>(n, 1) * sizeof(double)));
+  b.n = n;
+  return b.p;
+}
+
+void hipchk(hipError_t e, const char* what) {
+  if (e != hipSuccess)
+    throw Fail{JWV_ERR_DEVICE, std::string("HIP error: ") + hipGetErrorString(e) + " in " + what};
+}
+
+enum KernelKind {
+  K_FWT_FWD_TILE, K_FWT_FWD_RES, K_FWT_REV_TILE, K_FWT_REV_RES, K_WPT_FWD_TILE, K_WPT_FWD_RES,
+  K_WPT_REV_TILE, K_WPT_REV_RES, K_MODWT_FWD_TILE, K_MODWT_FWD_LEVEL, K_MODWT_INV_TILE,
+  K_MODWT_INV_LEVEL, K_COPY, K_NKINDS
+};
+const char* const kKindNames[K_NKINDS] = {
+    "fwt_fwd_tile", "fwt_fwd_res", "fwt_rev_tile", "fwt_rev_res", "wpt_fwd_tile", "wpt_fwd_res",
+    "wpt_rev_tile", "wpt_rev_res", "modwt_fwd_tile", "modwt_fwd_level", "modwt_inv_tile",
+    "modwt_inv_level", "copy_axis"};
+
+hipEvent_t take_event(jwv_ctx* c) {
+  if (!c->ev_pool.empty()) {
+    hipEvent_t e = c->ev_pool.back();
+    c->ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  hipchk(hipEventCreate(&e), "hipEventCreate");
+  return e;
+}
+
+// Brackets one kernel launch with events when profiling is on.  `bytes` is the
+// launch's algorithmic HBM traffic (compulsory reads + writes).
+struct ProfScope {
+  jwv_ctx* c;
+  bool on;
+  size_t idx = 0;
+  ProfScope(jwv_ctx* c_, int kind, double bytes) : c(c_), on(c_->prof) {
+    if (!on) return;
+    jwv_ctx::Rec r{kind, bytes, take_event(c), take_event(c)};
+    hipchk(hipEventRecord(r.e0, c->stream), "hipEventRecord");
+    c->recs.push_back(r);
+    idx = c->recs.size() - 1;
+  }
+  ~ProfScope() {
+    if (on) hipEventRecord(c->recs[idx].e1, c->stream);
+  }
+};
+
+struct Axis {
+  const double* src;
+  AxisView sv;
+  double* dst;
+  AxisView dv;
+  int64_t outer;
+  int len;
+  int inner;
+};
+
+bool use_fma(jwv_ctx* c) { return c->math == JWV_MATH_FMA; }
+
+void copy_axis(jwv_ctx* c, const Axis& a) {
+  { ProfScope ps_(c, K_COPY, 16.0 * a.outer * a.len * a.inner);
+    hipchk(jwv::launch_copy_axis(a.src, a.sv, a.dst, a.dv, a.outer, a.len, a.inner, c->stream),
+         "copy"); }
+}
+
+int col_slab(int inner) { return inner == 1 ? 1 : 8; }
+
+// Number of levels FastWaveletTransform / WaveletPacketTransform.forward runs
+// (FastWaveletTransform.java:90: while h >= transformWavelength && l < level).
+int fwd_levels(int len, int tw, int level) {
+  int h = len, l = 0;
+  while (h >= tw && l < level) { h >>= 1; ++l; }
+  return l;
+}
+// First reverse level size (FastWaveletTransform.java:137-141); 0 = none.
+int rev_first(int len, int tw, int level) {
+  const int steps = exponent(len);
+  int64_t h = tw;
+  for (int l = level; l < steps; ++l) h <<= 1;
+  return (h <= len && h >= tw) ? (int)h : 0;
+}
+
+// ------------------------------------------------------------------ FWT axis
+void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
+  const int nlev = fwd_levels(a.len, b.tw, level);
+  if (nlev == 0) return copy_axis(c, a);
+  const int C = col_slab(a.inner), cap = Geo::res_cap(C), KM = Geo::fwt_k(C);
+  // workspace: the largest intermediate approximation
+  {
+    int h = a.len, rem = nlev;
+    size_t need = 0;
+    while (rem > 0 && h > cap) {
+      const int K = std::min(rem, KM);
+      if (K < rem) need = std::max(need, (size_t)a.outer * (size_t)(h >> K) * a.inner);
+      h >>= K;
+      rem -= K;
+    }
+    if (need) { grow(c, c->ws[0], need); grow(c, c->ws[1], need); }
+  }
+  const double* cur = a.src;
+  AxisView cv = a.sv;
+  int h = a.len, rem = nlev, pp = 0;
+  while (rem > 0 && h > cap) {
+    const int K = std::min(rem, KM);
+    const bool last = K == rem;
+    double* ad = last ? a.dst : c->ws[pp].p;
+    const AxisView av = last ? a.dv : cview(h >> K, a.inner);
+    jwv::TileArgs t{cur, cv, nullptr, {}, a.dst, a.dv, ad, av, h, K, a.outer, a.inner};
+    { ProfScope ps_(c, K_FWT_FWD_TILE, 16.0 * a.outer * h * a.inner);
+    hipchk(jwv::launch_fwt_fwd_tile(b, use_fma(c), C, t, c->stream), "fwt_fwd_tile"); }
+    cur = ad;
+    cv = av;
+    h >>= K;
+    rem -= K;
+    pp ^= 1;
+  }
+  if (rem > 0) {
+    jwv::ResArgs r{cur, cv, a.dst, a.dv, h, 0, rem, a.outer, a.inner};
+    { ProfScope ps_(c, K_FWT_FWD_RES, 16.0 * a.outer * h * a.inner);
+    hipchk(jwv::launch_fwt_fwd_res(b, use_fma(c), C, r, c->stream), "fwt_fwd_res"); }
+  }
+}
+
+void fwt_rev_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
+  const int h = rev_first(a.len, b.tw, level);
+  if (h == 0) return copy_axis(c, a);
+  const int C = col_slab(a.inner), cap = Geo::res_cap(C), KM = Geo::fwt_k(C);
+  // workspace sizing
+  {
+    size_t need = 0;
+    int h1;
+    if (h <= cap) {
+      const int hres = std::min(a.len, cap);
+      if (hres < a.len) need = (size_t)a.outer * hres * a.inner;
+      h1 = hres * 2;
+    } else {
+      h1 = h;
+    }
+    while (h1 <= a.len) {
+      const int K = std::min(exponent(a.len / h1) + 1, KM);
+      const int hK = h1 << (K - 1);
+      if (hK < a.len) need = std::max(need, (size_t)a.outer * hK * a.inner);
+      h1 = hK * 2;
+    }
+    if (need) { grow(c, c->ws[0], need); grow(c, c->ws[1], need); }
+  }
+  const double* acur;
+  AxisView acv;
+  int h1, pp = 0;
+  if (h <= cap) {
+    const int hres = std::min(a.len, cap);
+    const int nres = exponent(hres / h) + 1;
+    const bool last = hres == a.len;
+    double* out = last ? a.dst : c->ws[pp].p;
+    const AxisView ov = last ? a.dv : cview(hres, a.inner);
+    jwv::ResArgs r{a.src, a.sv, out, ov, h, 0, nres, a.outer, a.inner};
+    { ProfScope ps_(c, K_FWT_REV_RES, 16.0 * a.outer * hres * a.inner);
+    hipchk(jwv::launch_fwt_rev_res(b, use_fma(c), C, r, c->stream), "fwt_rev_res"); }
+    if (last) return;
+    acur = out;
+    acv = ov;
+    h1 = hres * 2;
+    pp ^= 1;
+  } else {
+    acur = a.src;
+    acv = a.sv;
+    h1 = h;
+  }
+  while (h1 <= a.len) {
+    const int K = std::min(exponent(a.len / h1) + 1, KM);
+    const int hK = h1 << (K - 1);
+    const bool last = hK == a.len;
+    double* out = last ? a.dst : c->ws[pp].p;
+    const AxisView ov = last ? a.dv : cview(hK, a.inner);
+    jwv::TileArgs t{acur, acv, a.src, a.sv, out, ov, nullptr, {}, h1, K, a.outer, a.inner};
+    { ProfScope ps_(c, K_FWT_REV_TILE, 16.0 * a.outer * hK * a.inner);
+    hipchk(jwv::launch_fwt_rev_tile(b, use_fma(c), C, t, c->stream), "fwt_rev_tile"); }
+    acur = out;
+    acv = ov;
+    h1 = hK * 2;
+    pp ^= 1;
+  }
+}
+
+// ------------------------------------------------------------------ WPT axis
+struct WPass {
+  bool tiled;
+  int h;    // fwd: packet length at pass start; rev: packet length the pass works on
+  int h0;   // rev resident: first packet size
+  int nlev; // levels (K for tiled)
+  int pk;   // packets per signal
+};
+
+void run_wpt_passes(jwv_ctx* c, const Bank& b, const Axis& a, bool fwd,
+                    const std::vector<WPass>& ps) {
+  const int C = col_slab(a.inner);
+  const int P = (int)ps.size();
+  if (P > 1) grow(c, c->big2, (size_t)a.outer * a.len * a.inner);
+  const double* cur = a.src;
+  AxisView cv = a.sv;
+  for (int i = 0; i < P; ++i) {
+    const WPass& p = ps[i];
+    const bool to_dst = ((P - 1 - i) % 2) == 0;
+    double* out = to_dst ? a.dst : c->big2.p;
+    const AxisView ov = to_dst ? a.dv : cview(a.len, a.inner);
+    const AxisView sv = with_packets(cv, p.pk, p.h), dv = with_packets(ov, p.pk, p.h);
+    const int64_t nouter = a.outer * p.pk;
+    if (p.tiled) {
+      jwv::TileArgs t{cur, sv, nullptr, {}, out, dv, nullptr, {}, p.h, p.nlev, nouter, a.inner};
+      ProfScope ps_(c, fwd ? K_WPT_FWD_TILE : K_WPT_REV_TILE, 16.0 * a.outer * a.len * a.inner);
+      hipchk(fwd ? jwv::launch_wpt_fwd_tile(b, use_fma(c), C, t, c->stream)
+                 : jwv::launch_wpt_rev_tile(b, use_fma(c), C, t, c->stream),
+             "wpt_tile");
+    } else {
+      jwv::ResArgs r{cur, sv, out, dv, p.h, p.h0, p.nlev, nouter, a.inner};
+      ProfScope ps_(c, fwd ? K_WPT_FWD_RES : K_WPT_REV_RES, 16.0 * a.outer * a.len * a.inner);
+      hipchk(fwd ? jwv::launch_wpt_fwd_res(b, use_fma(c), C, r, c->stream)
+                 : jwv::launch_wpt_rev_res(b, use_fma(c), C, r, c->stream),
+             "wpt_res");
+    }
+    cur = out;
+    cv = ov;
+  }
+}
+
+void wpt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
+  const int nlev = fwd_levels(a.len, b.tw, level);
+  if (nlev == 0) return copy_axis(c, a);
+  const int C = col_slab(a.inner), cap = Geo::res_cap(C), KM = Geo::wpt_k(C);
+  std::vector<WPass> ps;
+  int h = a.len, pk = 1, rem = nlev;
+  while (rem > 0) {
+    if (h <= cap) {
+      ps.push_back({false, h, 0, rem, pk});
+      break;
+    }
+    const int K = std::min(rem, KM);
+    ps.push_back({true, h, 0, K, pk});
+    h >>= K;
+    pk <<= K;
+    rem -= K;
+  }
+  run_wpt_passes(c, b, a, true, ps);
+}
+
+void wpt_rev_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
+  const int h = rev_first(a.len, b.tw, level);
+  if (h == 0) return copy_axis(c, a);
+  const int C = col_slab(a.inner), cap = Geo::res_cap(C), KM = Geo::wpt_k(C);
+  std::vector<WPass> ps;
+  int h1;
+  if (h <= cap) {
+    const int hres = std::min(a.len, cap);
+    ps.push_back({false, hres, h, exponent(hres / h) + 1, a.len / hres});
+    h1 = hres * 2;
+  } else {
+    h1 = h;
+  }
+  while (h1 <= a.len) {
+    const int K = std::min(exponent(a.len / h1) + 1, KM);
+    const int hK = h1 << (K - 1);
+    ps.push_back({true, hK, 0, K, a.len / hK});
+    h1 = hK * 2;
+  }
+  run_wpt_passes(c, b, a, false, ps);
+}
+
+// ------------------------------------------------------------- validation
+enum class Kind { FWT, WPT };
+
+void check_1d(Kind k, bool fwd, int64_t n, int level) {
+  if (n > (int64_t(1) << 30))
+    throw Fail{JWV_ERR_BAD_CALL, "signal length exceeds the Java int array range (2^30)"};
+  const char* who = k == Kind::FWT ? (fwd ? "FastWaveletTransform#forward - "
+                                          : "FastWaveletTransform#reverse - ")
+                                   : "";
+  if (!is_binary(n))
+    throw Fail{JWV_ERR_FAILURE,
+               std::string(who) +
+                   "given array length is not 2^p | p E N ... = 1, 2, 4, 8, 16, 32, .. "
+                   "please use the Ancient Egyptian Decomposition for any other array length!"};
+  const int levels = exponent(n);
+  if (level < 0 || level > levels) {
+    if (k == Kind::FWT)
+      throw Fail{JWV_ERR_FAILURE, std::string(who) + "given level is out of range for given array"};
+    throw Fail{JWV_ERR_FAILURE, std::string("WaveletPacketTransform#") +
+                                    (fwd ? "forward" : "reverse") +
+                                    " - given level is out of range for given array"};
+  }
+}
+
+void check_ptrs(const void* x, const void* y) {
+  if (!x || !y) throw Fail{JWV_ERR_BAD_CALL, "NULL data pointer"};
+}
+
+void check_overlap(const double* x, size_t nx, const double* y, size_t ny) {
+  const char* xa = (const char*)x;
+  const char* ya = (const char*)y;
+  if (xa < ya + ny * sizeof(double) && ya < xa + nx * sizeof(double))
+    throw Fail{JWV_ERR_BAD_CALL, "output buffer overlaps input buffer"};
+}
+
+template <typename F>
+int guarded(jwv_ctx* c, F&& f) {
+  if (!c) return set_err(nullptr, JWV_ERR_BAD_CALL, "jwv_ctx is NULL");
+  std::lock_guard<std::mutex> lk(c->mu);
+  try {
+    c->err.clear();
+    hipchk(hipSetDevice(c->device), "hipSetDevice");
+    f();
+    return JWV_OK;
+  } catch (const Fail& e) {
+    return set_err(c, e.code, e.msg);
+  } catch (const std::exception& e) {
+    return set_err(c, JWV_ERR_DEVICE, e.what());
+  }
+}
+
+// Host-pointer wrapper: stage in / run device body / stage out, synchronous.
+template <typename Body>
+void staged(jwv_ctx* c, const double* x, size_t nx, double* y, size_t ny, Body&& body) {
+  double* dx = grow(c, c->hin, nx);
+  double* dy = grow(c, c->hout, ny);
+  hipchk(hipMemcpyAsync(dx, x, nx * sizeof(double), hipMemcpyHostToDevice, c->stream), "H2D");
+  body(dx, dy);
+  hipchk(hipMemcpyAsync(y, dy, ny * sizeof(double), hipMemcpyDeviceToHost, c->stream), "D2H");
+  hipchk(hipStreamSynchronize(c->stream), "sync");
+}
+
+// ----------------------------------------------------------------- bodies
+void body_1d(jwv_ctx* c, Kind k, bool fwd, const Bank& b, const double* x, double* y,
+             int64_t batch, int64_t n, int64_t ld, int level) {
+  if (batch == 0 || n == 0) return;
+  AxisView v{};
+  v.s_outer = ld;
+  v.s_len = 1;
+  v.pk = 1;
+  Axis a{x, v, y, v, batch, (int)n, 1};
+  if (k == Kind::FWT) (fwd ? fwt_fwd_axis : fwt_rev_axis)(c, b, a, level);
+  else (fwd ? wpt_fwd_axis : wpt_rev_axis)(c, b, a, level);
+}
+
+using AxisFn = void (*)(jwv_ctx*, const Bank&, const Axis&, int);
+
+AxisFn axis_fn(Kind k, bool fwd) {
+  if (k == Kind::FWT) return fwd ? fwt_fwd_axis : fwt_rev_axis;
+  return fwd ? wpt_fwd_axis : wpt_rev_axis;
+}
+
+// BasicTransform.java:361-399 (forward: rows lvlN -> columns lvlM) and
+// :436-474 (reverse: columns lvlM -> rows lvlN).
+void body_2d(jwv_ctx* c, Kind k, bool fwd, const Bank& b, const double* x, double* y,
+             int64_t rows, int64_t cols, int lvl_m, int lvl_n) {
+  if (rows == 0 || cols == 0) return;
+  double* tmp = grow(c, c->big, (size_t)(rows * cols));
+  const AxisView rv = cview(cols, 1), cvw = cview(rows, cols);
+  AxisFn f = axis_fn(k, fwd);
+  if (fwd) {
+    f(c, b, Axis{x, rv, tmp, rv, rows, (int)cols, 1}, lvl_n);
+    f(c, b, Axis{tmp, cvw, y, cvw, 1, (int)rows, (int)cols}, lvl_m);
+  } else {
+    f(c, b, Axis{x, cvw, tmp, cvw, 1, (int)rows, (int)cols}, lvl_m);
+    f(c, b, Axis{tmp, rv, y, rv, rows, (int)cols, 1}, lvl_n);
+  }
+}
+
+// BasicTransform.java:509-560 / 602-659: slice 2-D transform with (lvlP on the
+// Q axis, lvlQ on the R axis), then the P axis with lvlR.
+void body_3d(jwv_ctx* c, Kind k, bool fwd, const Bank& b, const double* x, double* y, int64_t P,
+             int64_t Q, int64_t R, int lvl_p, int lvl_q, int lvl_r) {
+  if (P == 0 || Q == 0 || R == 0) return;
+  double* tmp = grow(c, c->big, (size_t)(P * Q * R));
+  const AxisView vr = cview(R, 1), vq = cview(Q, R), vp = cview(P, Q * R);
+  AxisFn f = axis_fn(k, fwd);
+  if (fwd) {
+    f(c, b, Axis{x, vr, y, vr, P * Q, (int)R, 1}, lvl_q);          // rows of each slice
+    f(c, b, Axis{y, vq, tmp, vq, P, (int)Q, (int)R}, lvl_p);       // columns of each slice
+    f(c, b, Axis{tmp, vp, y, vp, 1, (int)P, (int)(Q * R)}, lvl_r); // along i
+  } else {
+    f(c, b, Axis{x, vq, y, vq, P, (int)Q, (int)R}, lvl_p);         // slice columns
+    f(c, b, Axis{y, vr, tmp, vr, P * Q, (int)R, 1}, lvl_q);        // slice rows
+    f(c, b, Axis{tmp, vp, y, vp, 1, (int)P, (int)(Q * R)}, lvl_r); // along i
+  }
+}
+
+// ------------------------------------------------------------------ MODWT
+// MODWTTransform.initializeFilterCache / normalize (MODWTTransform.java:452-484,
+// 599-606); evaluated in the same order, compiled with -ffp-contract=off.
+void modwt_filters(const Bank& b, double* g, double* h) {
+  auto normalize = [](double* f, int n) {
+    double energy = 0.0;
+    for (int i = 0; i < n; ++i) energy += f[i] * f[i];
+    const double norm = std::sqrt(energy);
+    if (norm > 1e-12)
+      for (int i = 0; i < n; ++i) f[i] /= norm;
+  };
+  for (int i = 0; i < b.L; ++i) { g[i] = b.lo[i]; h[i] = b.hi[i]; }
+  normalize(g, b.L);
+  normalize(h, b.L);
+  const double s = std::sqrt(2.0);
+  for (int i = 0; i < b.L; ++i) { g[i] = g[i] / s; h[i] = h[i] / s; }
+}
+
+Bank modwt_bank(const Bank& b) {
+  Bank m;
+  m.L = b.L;
+  modwt_filters(b, m.lo, m.hi);
+  return m;
+}
+
+void check_modwt(int64_t n, int J) {
+  // MODWTTransform.forwardMODWT checks, :257-282
+  if (J < 1)
+    throw Fail{JWV_ERR_ILLEGAL_ARGUMENT,
+               "MODWTTransform#forwardMODWT - decomposition level must be at least 1, requested: " +
+                   std::to_string(J)};
+  if (J > 13)
+    throw Fail{JWV_ERR_ILLEGAL_ARGUMENT,
+               "MODWTTransform#forwardMODWT - maximum supported decomposition level is 13, "
+               "requested: " + std::to_string(J)};
+  if (n > 0x7fffffffLL) throw Fail{JWV_ERR_BAD_CALL, "signal length exceeds int range"};
+  if (n > 0) {
+    int theo = 0;
+    while ((int64_t(1) << (theo + 1)) <= n) ++theo;
+    if (J > theo)
+      throw Fail{JWV_ERR_ILLEGAL_ARGUMENT, "Decomposition level " + std::to_string(J) +
+                                               " exceeds theoretical limit " +
+                                               std::to_string(theo) + " for signal length " +
+                                               std::to_string(n)};
+  }
+}
+
+int64_t modwt_halo(int L, int j0, int j1) {
+  return (int64_t)(L - 1) * ((int64_t(1) << j1) - (int64_t(1) << (j0 - 1)));
+}
+
+void body_modwt_fwd(jwv_ctx* c, const Bank& b, const double* x, double* wv, int64_t N, int J) {
+  if (N == 0) return;
+  const Bank m = modwt_bank(b);
+  grow(c, c->ws[0], (size_t)N);
+  grow(c, c->ws[1], (size_t)N);
+  const double* vin = x;
+  int pp = 0, j0 = 1;
+  while (j0 <= J) {
+    int j1 = j0 - 1;
+    while (j1 + 1 <= J && modwt_halo(m.L, j0, j1 + 1) <= Geo::kModS) ++j1;
+    const bool tiled = j1 >= j0;
+    if (!tiled) j1 = j0;
+    double* vout = (j1 == J) ? wv + (int64_t)J * N : c->ws[pp].p;
+    jwv::ModwtArgs a{vin, nullptr, wv, vout, N, N, j0, j1};
+    {
+      ProfScope ps_(c, tiled ? K_MODWT_FWD_TILE : K_MODWT_FWD_LEVEL,
+                    8.0 * N * (1 + (j1 - j0 + 1) + 1));
+      hipchk(jwv::launch_modwt_fwd(m, use_fma(c), tiled, a, c->stream), "modwt_fwd");
+    }
+    vin = vout;
+    pp ^= 1;
+    j0 = j1 + 1;
+  }
+}
+
+void body_modwt_inv(jwv_ctx* c, const Bank& b, const double* wv, double* x, int64_t N, int J) {
+  if (N == 0 || J < 1) return;
+  const Bank m = modwt_bank(b);
+  grow(c, c->ws[0], (size_t)N);
+  grow(c, c->ws[1], (size_t)N);
+  const double* vin = wv + (int64_t)J * N;
+  int pp = 0, j1 = J;
+  while (j1 >= 1) {
+    int j0 = j1 + 1;
+    while (j0 - 1 >= 1 && modwt_halo(m.L, j0 - 1, j1) <= Geo::kModS) --j0;
+    const bool tiled = j0 <= j1;
+    if (!tiled) j0 = j1;
+    double* vout = (j0 == 1) ? x : c->ws[pp].p;
+    jwv::ModwtArgs a{vin, wv, nullptr, vout, N, N, j0, j1};
+    {
+      ProfScope ps_(c, tiled ? K_MODWT_INV_TILE : K_MODWT_INV_LEVEL,
+                    8.0 * N * (1 + (j1 - j0 + 1) + 1));
+      hipchk(jwv::launch_modwt_inv(m, use_fma(c), tiled, a, c->stream), "modwt_inv");
+    }
+    vin = vout;
+    pp ^= 1;
+    j1 = j0 - 1;
+  }
+}
+
+void need_device_ptrs(const double* x, const double* y) { check_ptrs(x, y); }
+
+}  // namespace
+
+// dispatch shims for the two math modes
+namespace jwv {
+#define JWV_MODE2(name, ...) \
+  return fma ? fused::name(__VA_ARGS__) : exact::name(__VA_ARGS__)
+hipError_t launch_fwt_fwd_res(const Bank& b, bool fma, int C, const ResArgs& a, hipStream_t s) {
+  JWV_MODE2(fwt_fwd_res, b, C, a, s);
+}
+hipError_t launch_fwt_rev_res(const Bank& b, bool fma, int C, const ResArgs& a, hipStream_t s) {
+  JWV_MODE2(fwt_rev_res, b, C, a, s);
+}
+hipError_t launch_fwt_fwd_tile(const Bank& b, bool fma, int C, const TileArgs& a, hipStream_t s) {
+  JWV_MODE2(fwt_fwd_tile, b, C, a, s);
+}
+hipError_t launch_fwt_rev_tile(const Bank& b, bool fma, int C, const TileArgs& a, hipStream_t s) {
+  JWV_MODE2(fwt_rev_tile, b, C, a, s);
+}
+hipError_t launch_wpt_fwd_res(const Bank& b, bool fma, int C, const ResArgs& a, hipStream_t s) {
+  JWV_MODE2(wpt_fwd_res, b, C, a, s);
+}
+hipError_t launch_wpt_rev_res(const Bank& b, bool fma, int C, const ResArgs& a, hipStream_t s) {
+  JWV_MODE2(wpt_rev_res, b, C, a, s);
+}
+hipError_t launch_wpt_fwd_tile(const Bank& b, bool fma, int C, const TileArgs& a, hipStream_t s) {
+  JWV_MODE2(wpt_fwd_tile, b, C, a, s);
+}
+hipError_t launch_wpt_rev_tile(const Bank& b, bool fma, int C, const TileArgs& a, hipStream_t s) {
+  JWV_MODE2(wpt_rev_tile, b, C, a, s);
+}
+hipError_t launch_modwt_fwd(const Bank& b, bool fma, bool tiled, const ModwtArgs& a,
+                            hipStream_t s) {
+  JWV_MODE2(modwt_fwd, b, tiled, a, s);
+}
+hipError_t launch_modwt_inv(const Bank& b, bool fma, bool tiled, const ModwtArgs& a,
+                            hipStream_t s) {
+  JWV_MODE2(modwt_inv, b, tiled, a, s);
+}
+}  // namespace jwv
+
+// =================================================================== C ABI
+extern "C" {
+
+int jwv_version(void) { return 100; }
+
+int jwv_ctx_create(int device, jwv_ctx** out) {
+  if (!out) return set_err(nullptr, JWV_ERR_BAD_CALL, "out is NULL");
+  *out = nullptr;
+  int count = 0;
+  hipError_t e = hipGetDeviceCount(&count);
+  if (e != hipSuccess || count == 0)
+    return set_err(nullptr, JWV_ERR_DEVICE,
+                   std::string("no HIP device available: ") + hipGetErrorString(e));
+  if (device < 0 || device >= count)
+    return set_err(nullptr, JWV_ERR_BAD_CALL, "device index out of range");
+  if ((e = hipSetDevice(device)) != hipSuccess)
+    return set_err(nullptr, JWV_ERR_DEVICE, hipGetErrorString(e));
+  jwv_ctx* c = new jwv_ctx();
+  c->device = device;
+  if ((e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking)) != hipSuccess) {
+    delete c;
+    return set_err(nullptr, JWV_ERR_DEVICE, hipGetErrorString(e));
+  }
+  c->stream = c->own;
+  *out = c;
+  return JWV_OK;
+}
+
+int jwv_ctx_destroy(jwv_ctx* c) {
+  if (!c) return JWV_OK;
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->stream);
+  for (DevBuf* b : {&c->ws[0], &c->ws[1], &c->big, &c->big2, &c->hin, &c->hout})
+    if (b->p) hipFree(b->p);
+  for (auto& r : c->recs) { hipEventDestroy(r.e0); hipEventDestroy(r.e1); }
+  for (auto e : c->ev_pool) hipEventDestroy(e);
+  if (c->own) hipStreamDestroy(c->own);
+  delete c;
+  return JWV_OK;
+}
+
+const char* jwv_last_error(const jwv_ctx* c) { return c ? c->err.c_str() : g_tls_error.c_str(); }
+
+int jwv_ctx_set_stream(jwv_ctx* c, void* s) {
+  if (!c) return set_err(nullptr, JWV_ERR_BAD_CALL, "jwv_ctx is NULL");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->stream = s ? (hipStream_t)s : c->own;
+  return JWV_OK;
+}
+
+void* jwv_ctx_get_stream(const jwv_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int jwv_ctx_set_math(jwv_ctx* c, int mode) {
+  if (!c) return set_err(nullptr, JWV_ERR_BAD_CALL, "jwv_ctx is NULL");
+  if (mode != JWV_MATH_EXACT && mode != JWV_MATH_FMA)
+    return set_err(c, JWV_ERR_BAD_CALL, "unknown math mode");
+  c->math = mode;
+  return JWV_OK;
+}
+
+int jwv_ctx_synchronize(jwv_ctx* c) {
+  return guarded(c, [&] { hipchk(hipStreamSynchronize(c->stream), "sync"); });
+}
+
+int jwv_ctx_profile_enable(jwv_ctx* c, int on) {
+  if (!c) return set_err(nullptr, JWV_ERR_BAD_CALL, "jwv_ctx is NULL");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->prof = on != 0;
+  return JWV_OK;
+}
+
+int jwv_ctx_profile_read(jwv_ctx* c, jwv_kernel_stat* out, int max_out, int* n_out) {
+  return guarded(c, [&] {
+    hipchk(hipStreamSynchronize(c->stream), "sync");
+    jwv_kernel_stat acc[K_NKINDS];
+    std::memset(acc, 0, sizeof(acc));
+    for (auto& r : c->recs) {
+      float ms = 0.f;
+      hipchk(hipEventElapsedTime(&ms, r.e0, r.e1), "hipEventElapsedTime");
+      acc[r.kind].launches += 1;
+      acc[r.kind].total_ms += ms;
+      acc[r.kind].bytes += r.bytes;
+      c->ev_pool.push_back(r.e0);
+      c->ev_pool.push_back(r.e1);
+    }
+    c->recs.clear();
+    int n = 0;
+    for (int k = 0; k < K_NKINDS; ++k) {
+      if (acc[k].launches == 0) continue;
+      std::snprintf(acc[k].name, sizeof(acc[k].name), "%s", kKindNames[k]);
+      if (out && n < max_out) out[n] = acc[k];
+      ++n;
+    }
+    if (n_out) *n_out = n;
+  });
+}
+
+int jwv_ctx_trim(jwv_ctx* c) {
+  return guarded(c, [&] {
+    hipchk(hipStreamSynchronize(c->stream), "sync");
+    for (DevBuf* b : {&c->ws[0], &c->ws[1], &c->big, &c->big2, &c->hin, &c->hout}) {
+      if (b->p) hipchk(hipFree(b->p), "free");
+      b->p = nullptr;
+      b->n = 0;
+    }
+  });
+}
+
+// ---- 1-D FWT / WPT ----------------------------------------------------------
+#define JWV_1D(NAME, KIND, FWD)                                                                \
+  int NAME(const double* x, double* y, int64_t n, int level, const jwv_taps* t, jwv_ctx* c) { \
+    return guarded(c, [&] {                                                                    \
+      const Bank b = make_bank(t);                                                             \
+      check_1d(KIND, FWD, n, level);                                                           \
+      check_ptrs(x, y);                                                                        \
+      staged(c, x, (size_t)n, y, (size_t)n, [&](const double* dx, double* dy) {               \
+        body_1d(c, KIND, FWD, b, dx, dy, 1, n, n, level);                                      \
+      });                                                                                      \
+    });                                                                                        \
+  }                                                                                            \
+  int NAME##_dev(const double* x, double* y, int64_t n, int level, const jwv_taps* t,          \
+                 jwv_ctx* c) {                                                                 \
+    return guarded(c, [&] {                                                                    \
+      const Bank b = make_bank(t);                                                             \
+      check_1d(KIND, FWD, n, level);                                                           \
+      need_device_ptrs(x, y);                                                                  \
+      check_overlap(x, (size_t)n, y, (size_t)n);                                               \
+      body_1d(c, KIND, FWD, b, x, y, 1, n, n, level);                                          \
+    });                                                                                        \
+  }
+JWV_1D(jwv_fwt_fwd_f64, Kind::FWT, true)
+JWV_1D(jwv_fwt_rev_f64, Kind::FWT, false)
+JWV_1D(jwv_wpt_fwd_f64, Kind::WPT, true)
+JWV_1D(jwv_wpt_rev_f64, Kind::WPT, false)
+
+#define JWV_BATCH(NAME, KIND, FWD)                                                              \
+  int NAME(const double* x, double* y, int64_t batch, int64_t n, int64_t ld, int level,         \
+           const jwv_taps* t, jwv_ctx* c) {                                                     \
+    return guarded(c, [&] {                                                                     \
+      const Bank b = make_bank(t);                                                              \
+      if (batch < 0 || ld < n) throw Fail{JWV_ERR_BAD_CALL, "batch < 0 or ld < n"};             \
+      check_1d(KIND, FWD, n, level);                                                            \
+      if (batch == 0) return;                                                                   \
+      check_ptrs(x, y);                                                                         \
+      const size_t tot = (size_t)((batch - 1) * ld + n);                                        \
+      staged(c, x, tot, y, tot, [&](const double* dx, double* dy) {                            \
+        body_1d(c, KIND, FWD, b, dx, dy, batch, n, ld, level);                                  \
+      });                                                                                       \
+    });                                                                                         \
+  }                                                                                             \
+  int NAME##_dev(const double* x, double* y, int64_t batch, int64_t n, int64_t ld, int level,   \
+                 const jwv_taps* t, jwv_ctx* c) {                                               \
+    return guarded(c, [&] {                                                                     \
+      const Bank b = make_bank(t);                                                              \
+      if (batch < 0 || ld < n) throw Fail{JWV_ERR_BAD_CALL, "batch < 0 or ld < n"};             \
+      check_1d(KIND, FWD, n, level);                                                            \
+      if (batch == 0) return;                                                                   \
+      need_device_ptrs(x, y);                                                                   \
+      const size_t tot = (size_t)((batch - 1) * ld + n);                                        \
+      check_overlap(x, tot, y, tot);                                                            \
+      body_1d(c, KIND, FWD, b, x, y, batch, n, ld, level);                                      \
+    });                                                                                         \
+  }
+JWV_BATCH(jwv_fwt_fwd_batch_f64, Kind::FWT, true)
+JWV_BATCH(jwv_fwt_rev_batch_f64, Kind::FWT, false)
+JWV_BATCH(jwv_wpt_fwd_batch_f64, Kind::WPT, true)
+JWV_BATCH(jwv_wpt_rev_batch_f64, Kind::WPT, false)
+
+// ---- 2-D / 3-D -------------------------------------------------------------------
+static void check_2d(Kind k, bool fwd, int64_t rows, int64_t cols, int lvl_m, int lvl_n) {
+  if (rows < 0 || cols < 0) throw Fail{JWV_ERR_BAD_CALL, "negative dimension"};
+  if (rows == 0 || cols == 0) return;
+  // forward validates rows first (row pass), reverse the columns first
+  if (fwd) { check_1d(k, true, cols, lvl_n); check_1d(k, true, rows, lvl_m); }
+  else { check_1d(k, false, rows, lvl_m); check_1d(k, false, cols, lvl_n); }
+  if (rows * cols > (int64_t(1) << 33)) throw Fail{JWV_ERR_BAD_CALL, "matrix too large"};
+}
+
+#define JWV_2D(NAME, KIND, FWD)                                                                  \
+  int NAME(const double* x, double* y, int64_t rows, int64_t cols, int lvl_m, int lvl_n,         \
+           const jwv_taps* t, jwv_ctx* c) {                                                      \
+    return guarded(c, [&] {                                                                      \
+      const Bank b = make_bank(t);                                                               \
+      check_2d(KIND, FWD, rows, cols, lvl_m, lvl_n);                                             \
+      if (rows == 0 || cols == 0) return;                                                        \
+      check_ptrs(x, y);                                                                          \
+      const size_t tot = (size_t)(rows * cols);                                                  \
+      staged(c, x, tot, y, tot, [&](const double* dx, double* dy) {                              \
+        body_2d(c, KIND, FWD, b, dx, dy, rows, cols, lvl_m, lvl_n);                              \
+      });                                                                                        \
+    });                                                                                          \
+  }
+#define JWV_2D_DEV(NAME, KIND, FWD)                                                              \
+  int NAME(const double* x, double* y, int64_t rows, int64_t cols, int lvl_m, int lvl_n,         \
+           const jwv_taps* t, jwv_ctx* c) {                                                      \
+    return guarded(c, [&] {                                                                      \
+      const Bank b = make_bank(t);                                                               \
+      check_2d(KIND, FWD, rows, cols, lvl_m, lvl_n);                                             \
+      if (rows == 0 || cols == 0) return;                                                        \
+      need_device_ptrs(x, y);                                                                    \
+      check_overlap(x, (size_t)(rows * cols), y, (size_t)(rows * cols));                         \
+      body_2d(c, KIND, FWD, b, x, y, rows, cols, lvl_m, lvl_n);                                  \
+    });                                                                                          \
+  }
+JWV_2D(jwv_fwt2d_fwd_f64, Kind::FWT, true)
+JWV_2D(jwv_fwt2d_rev_f64, Kind::FWT, false)
+JWV_2D_DEV(jwv_fwt2d_fwd_f64_dev, Kind::FWT, true)
+JWV_2D_DEV(jwv_fwt2d_rev_f64_dev, Kind::FWT, false)
+JWV_2D(jwv_wpt2d_fwd_f64, Kind::WPT, true)
+JWV_2D(jwv_wpt2d_rev_f64, Kind::WPT, false)
+JWV_2D_DEV(jwv_wpt2d_fwd_f64_dev, Kind::WPT, true)
+JWV_2D_DEV(jwv_wpt2d_rev_f64_dev, Kind::WPT, false)
+
+static void check_3d(Kind k, bool fwd, int64_t P, int64_t Q, int64_t R, int lp, int lq, int lr) {
+  if (P < 0 || Q < 0 || R < 0) throw Fail{JWV_ERR_BAD_CALL, "negative dimension"};
+  if (P == 0 || Q == 0 || R == 0) return;
+  if (fwd) {
+    check_1d(k, true, R, lq);
+    check_1d(k, true, Q, lp);
+    check_1d(k, true, P, lr);
+  } else {
+    check_1d(k, false, Q, lp);
+    check_1d(k, false, R, lq);
+    check_1d(k, false, P, lr);
+  }
+  if (P * Q * R > (int64_t(1) << 33)) throw Fail{JWV_ERR_BAD_CALL, "volume too large"};
+}
+
+#define JWV_3D(NAME, KIND, FWD, DEV)                                                                    \
+  int NAME(const double* x, double* y, int64_t P, int64_t Q, int64_t R, int lp, int lq, int lr,   \
+           const jwv_taps* t, jwv_ctx* c) {                                                       \
+    return guarded(c, [&] {                                                                       \
+      const Bank b = make_bank(t);                                                                \
+      check_3d(KIND, FWD, P, Q, R, lp, lq, lr);                                                         \
+      if (P == 0 || Q == 0 || R == 0) return;                                                     \
+      check_ptrs(x, y);                                                                           \
+      const size_t tot = (size_t)(P * Q * R);                                                     \
+      if (DEV) {                                                                                  \
+        check_overlap(x, tot, y, tot);                                                            \
+        body_3d(c, KIND, FWD, b, x, y, P, Q, R, lp, lq, lr);                                      \
+      } else {                                                                                    \
+        staged(c, x, tot, y, tot, [&](const double* dx, double* dy) {                             \
+          body_3d(c, KIND, FWD, b, dx, dy, P, Q, R, lp, lq, lr);                                  \
+        });                                                                                       \
+      }                                                                                           \
+    });                                                                                           \
+  }
+JWV_3D(jwv_fwt3d_fwd_f64, Kind::FWT, true, false)
+JWV_3D(jwv_fwt3d_rev_f64, Kind::FWT, false, false)
+JWV_3D(jwv_fwt3d_fwd_f64_dev, Kind::FWT, true, true)
+JWV_3D(jwv_fwt3d_rev_f64_dev, Kind::FWT, false, true)
+JWV_3D(jwv_wpt3d_fwd_f64, Kind::WPT, true, false)
+JWV_3D(jwv_wpt3d_rev_f64, Kind::WPT, false, false)
+
+// ---- MODWT -------------------------------------------------------------------------
+int jwv_modwt_filters(const jwv_taps* t, double* g, double* h) {
+  try {
+    const Bank b = make_bank(t);
+    if (!g || !h) throw Fail{JWV_ERR_BAD_CALL, "NULL output"};
+    modwt_filters(b, g, h);
+    return JWV_OK;
+  } catch (const Fail& e) {
+    return set_err(nullptr, e.code, e.msg);
+  }
+}
+
+int jwv_modwt_fwd_f64(const double* x, double* wv, int64_t n, int J, const jwv_taps* t,
+                      jwv_ctx* c) {
+  return guarded(c, [&] {
+    const Bank b = make_bank(t);
+    check_modwt(n, J);
+    if (n == 0) return;
+    check_ptrs(x, wv);
+    staged(c, x, (size_t)n, wv, (size_t)n * (J + 1),
+           [&](const double* dx, double* dy) { body_modwt_fwd(c, b, dx, dy, n, J); });
+  });
+}
+int jwv_modwt_fwd_f64_dev(const double* x, double* wv, int64_t n, int J, const jwv_taps* t,
+                          jwv_ctx* c) {
+  return guarded(c, [&] {
+    const Bank b = make_bank(t);
+    check_modwt(n, J);
+    if (n == 0) return;
+    need_device_ptrs(x, wv);
+    check_overlap(x, (size_t)n, wv, (size_t)n * (J + 1));
+    body_modwt_fwd(c, b, x, wv, n, J);
+  });
+}
+// MODWTTransform.inverseMODWT: coefficients.length <= 1 -> empty (:338-346).
+int jwv_modwt_inv_f64(const double* wv, double* x, int64_t n, int J, const jwv_taps* t,
+                      jwv_ctx* c) {
+  return guarded(c, [&] {
+    const Bank b = make_bank(t);
+    if (J < 1 || n == 0) return;
+    if (J > 13 || n > 0x7fffffffLL) throw Fail{JWV_ERR_BAD_CALL, "J > 13 or n too large"};
+    check_ptrs(wv, x);
+    staged(c, wv, (size_t)n * (J + 1), x, (size_t)n,
+           [&](const double* dx, double* dy) { body_modwt_inv(c, b, dx, dy, n, J); });
+  });
+}
+int jwv_modwt_inv_f64_dev(const double* wv, double* x, int64_t n, int J, const jwv_taps* t,
+                          jwv_ctx* c) {
+  return guarded(c, [&] {
+    const Bank b = make_bank(t);
+    if (J < 1 || n == 0) return;
+    if (J > 13 || n > 0x7fffffffLL) throw Fail{JWV_ERR_BAD_CALL, "J > 13 or n too large"};
+    need_device_ptrs(wv, x);
+    check_overlap(wv, (size_t)n * (J + 1), x, (size_t)n);
+    body_modwt_inv(c, b, wv, x, n, J);
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,121 @@
+// jwv_launch.hpp — host-side launch interface between the C-ABI planner
+// (capi.cpp) and the kernel translation units (launch_*.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "jwv_device.hpp"
+
+namespace jwv {
+
+// Host copy of a filter bank (Wavelet getters, Wavelet.java:152-219).
+struct Bank {
+  int L = 0;
+  int tw = 2;
+  double lo[kMaxTaps] = {};
+  double hi[kMaxTaps] = {};
+  double lo_r[kMaxTaps] = {};
+  double hi_r[kMaxTaps] = {};
+  double scale = 1.0;  // Haar1Orthogonal reverse factor
+};
+
+// Tap counts with compiled-in (unrolled, SGPR-resident) kernels; every other
+// bank runs the runtime-L kernels (L=0 instantiation).
+inline int static_l(int L) {
+  switch (L) {
+    case 2: case 4: case 8: case 16: return L;
+    default: return 0;
+  }
+}
+
+struct ResArgs {  // resident FWT/WPT kernels
+  const double* src; AxisView sv;
+  double* dst; AxisView dv;
+  int n;       // FWT fwd: h0 (level input length); FWT rev: h0; WPT: signal/packet length
+  int h0;      // WPT rev: first packet size
+  int nlev;
+  int64_t nouter;
+  int inner;
+};
+struct TileArgs {  // tiled FWT/WPT kernels
+  const double* src; AxisView sv;   // level input (fwd) / approximation (FWT rev) / bands (WPT rev)
+  const double* coef; AxisView cv;  // FWT rev: coefficient array
+  double* dst; AxisView dv;
+  double* adst; AxisView av;        // FWT fwd: level-K approximation
+  int h;       // FWT/WPT fwd: level input length; FWT rev: h1; WPT rev: hK
+  int K;
+  int64_t nouter;
+  int inner;
+};
+struct ModwtArgs {
+  const double* src;  // fwd: V_{j0-1}; inv: V_{j1}
+  const double* coef; // inv: W rows base
+  double* wout;       // fwd: W rows base
+  double* vout;       // fwd: V_{j1}; inv: V_{j0-1}
+  int64_t ldw;
+  int64_t N;
+  int j0, j1;
+};
+
+// Geometry of the compiled kernels (must match the template arguments used
+// in launch_*.hip).  C = column slab: 1 for contiguous signals, 8 otherwise.
+struct Geo {
+  static constexpr int NT = 256;
+  static constexpr int kResCap1 = 8192;  // resident elements per column, C = 1
+  static constexpr int kResCap8 = 1024;  // C = 8
+  static constexpr int kFwtT1 = 4096, kFwtK1 = 6;
+  static constexpr int kFwtT8 = 512, kFwtK8 = 3;
+  static constexpr int kWptT1 = 8192, kWptK1 = 6;
+  static constexpr int kWptT8 = 512, kWptK8 = 3;
+  static constexpr int kModT = 4096, kModS = 2048;
+  static int res_cap(int C) { return C == 1 ? kResCap1 : kResCap8; }
+  static int fwt_t(int C) { return C == 1 ? kFwtT1 : kFwtT8; }
+  static int fwt_k(int C) { return C == 1 ? kFwtK1 : kFwtK8; }
+  static int wpt_t(int C) { return C == 1 ? kWptT1 : kWptT8; }
+  static int wpt_k(int C) { return C == 1 ? kWptK1 : kWptK8; }
+};
+
+// Each returns hipSuccess or the launch error.  `fma` selects the math mode.
+hipError_t launch_fwt_fwd_res(const Bank&, bool fma, int C, const ResArgs&, hipStream_t);
+hipError_t launch_fwt_rev_res(const Bank&, bool fma, int C, const ResArgs&, hipStream_t);
+hipError_t launch_fwt_fwd_tile(const Bank&, bool fma, int C, const TileArgs&, hipStream_t);
+hipError_t launch_fwt_rev_tile(const Bank&, bool fma, int C, const TileArgs&, hipStream_t);
+hipError_t launch_wpt_fwd_res(const Bank&, bool fma, int C, const ResArgs&, hipStream_t);
+hipError_t launch_wpt_rev_res(const Bank&, bool fma, int C, const ResArgs&, hipStream_t);
+hipError_t launch_wpt_fwd_tile(const Bank&, bool fma, int C, const TileArgs&, hipStream_t);
+hipError_t launch_wpt_rev_tile(const Bank&, bool fma, int C, const TileArgs&, hipStream_t);
+hipError_t launch_modwt_fwd(const Bank& modwt_gh, bool fma, bool tiled, const ModwtArgs&,
+                            hipStream_t);
+hipError_t launch_modwt_inv(const Bank& modwt_gh, bool fma, bool tiled, const ModwtArgs&,
+                            hipStream_t);
+hipError_t launch_copy_axis(const double* src, AxisView sv, double* dst, AxisView dv,
+                            int64_t nouter, int len, int inner, hipStream_t);
+
+// Per-mode entry points implemented by launch_{fwt,wpt,modwt}.hip compiled
+// twice (JWV_FMA=0 / 1).
+namespace exact {
+hipError_t fwt_fwd_res(const Bank&, int C, const ResArgs&, hipStream_t);
+hipError_t fwt_rev_res(const Bank&, int C, const ResArgs&, hipStream_t);
+hipError_t fwt_fwd_tile(const Bank&, int C, const TileArgs&, hipStream_t);
+hipError_t fwt_rev_tile(const Bank&, int C, const TileArgs&, hipStream_t);
+hipError_t wpt_fwd_res(const Bank&, int C, const ResArgs&, hipStream_t);
+hipError_t wpt_rev_res(const Bank&, int C, const ResArgs&, hipStream_t);
+hipError_t wpt_fwd_tile(const Bank&, int C, const TileArgs&, hipStream_t);
+hipError_t wpt_rev_tile(const Bank&, int C, const TileArgs&, hipStream_t);
+hipError_t modwt_fwd(const Bank&, bool tiled, const ModwtArgs&, hipStream_t);
+hipError_t modwt_inv(const Bank&, bool tiled, const ModwtArgs&, hipStream_t);
+}  // namespace exact
+namespace fused {
+hipError_t fwt_fwd_res(const Bank&, int C, const ResArgs&, hipStream_t);
+hipError_t fwt_rev_res(const Bank&, int C, const ResArgs&, hipStream_t);
+hipError_t fwt_fwd_tile(const Bank&, int C, const TileArgs&, hipStream_t);
+hipError_t fwt_rev_tile(const Bank&, int C, const TileArgs&, hipStream_t);
+hipError_t wpt_fwd_res(const Bank&, int C, const ResArgs&, hipStream_t);
+hipError_t wpt_rev_res(const Bank&, int C, const ResArgs&, hipStream_t);
+hipError_t wpt_fwd_tile(const Bank&, int C, const TileArgs&, hipStream_t);
+hipError_t wpt_rev_tile(const Bank&, int C, const TileArgs&, hipStream_t);
+hipError_t modwt_fwd(const Bank&, bool tiled, const ModwtArgs&, hipStream_t);
+hipError_t modwt_inv(const Bank&, bool tiled, const ModwtArgs&, hipStream_t);
+}  // namespace fused
+
+}  // namespace jwv

@@ -1,0 +1,214 @@
+// launch_fwt_wpt.hip — instantiates the FWT / WPT kernels for one math mode.
+// Compiled twice: -DJWV_FMA=0 (namespace jwv::exact) and -DJWV_FMA=1
+// (namespace jwv::fused).  Grid/LDS geometry comes from jwv::Geo.
+#include "jwv_launch.hpp"
+#include "wpt_kernels.hpp"
+
+#ifndef JWV_FMA
+#error "JWV_FMA must be 0 or 1"
+#endif
+#if JWV_FMA
+#define JWV_NS fused
+#else
+#define JWV_NS exact
+#endif
+
+namespace jwv {
+namespace {
+constexpr bool kFMA = JWV_FMA != 0;
+constexpr int NT = Geo::NT;
+
+template <int L>
+FwdTaps<L> fwd_taps_s(const Bank& b) {
+  FwdTaps<L> t;
+  for (int j = 0; j < L; ++j) { t.lo[j] = b.lo[j]; t.hi[j] = b.hi[j]; }
+  return t;
+}
+template <int L>
+RevTaps<L> rev_taps_s(const Bank& b) {
+  RevTaps<L> t;
+  for (int j = 0; j < L; ++j) { t.lo_r[j] = b.lo_r[j]; t.hi_r[j] = b.hi_r[j]; }
+  return t;
+}
+AnyTaps any_taps(const Bank& b) {
+  AnyTaps t{};
+  for (int j = 0; j < b.L; ++j) {
+    t.lo[j] = b.lo[j]; t.hi[j] = b.hi[j]; t.lo_r[j] = b.lo_r[j]; t.hi_r[j] = b.hi_r[j];
+  }
+  t.scale = b.scale;
+  t.L = b.L;
+  return t;
+}
+template <int L>
+typename FB<L>::Fwd fwd_taps(const Bank& b) {
+  if constexpr (L == 0) return any_taps(b); else return fwd_taps_s<L>(b);
+}
+template <int L>
+typename FB<L>::Rev rev_taps(const Bank& b) {
+  if constexpr (L == 0) return any_taps(b); else return rev_taps_s<L>(b);
+}
+
+template <typename K>
+hipError_t prep(K kernel, size_t lds) {
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+template <int C> constexpr int cap() { return C == 1 ? Geo::kResCap1 : Geo::kResCap8; }
+template <int C> constexpr int fwt_T() { return C == 1 ? Geo::kFwtT1 : Geo::kFwtT8; }
+template <int C> constexpr int fwt_K() { return C == 1 ? Geo::kFwtK1 : Geo::kFwtK8; }
+template <int C> constexpr int wpt_T() { return C == 1 ? Geo::kWptT1 : Geo::kWptT8; }
+template <int C> constexpr int wpt_K() { return C == 1 ? Geo::kWptK1 : Geo::kWptK8; }
+inline unsigned ncb(int inner, int C) { return (unsigned)((inner + C - 1) / C); }
+
+// ------------------------------------------------------------- FWT
+template <int L, int C>
+hipError_t fwt_fwd_res_go(const Bank& b, const ResArgs& a, hipStream_t s) {
+  auto k = fwt_fwd_res<L, C, NT, cap<C>(), kFMA>;
+  const size_t lds = (size_t)a.n * C * sizeof(double);
+  if (hipError_t e = prep(k, lds)) return e;
+  const dim3 grid((unsigned)(a.nouter * ncb(a.inner, C)));
+  hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.sv, a.dst, a.dv, a.n, a.nlev, a.inner,
+                     fwd_taps<L>(b));
+  return hipGetLastError();
+}
+template <int L, int C>
+hipError_t fwt_rev_res_go(const Bank& b, const ResArgs& a, hipStream_t s) {
+  auto k = fwt_rev_res<L, C, NT, cap<C>(), kFMA>;
+  const int htop = a.nlev > 0 ? (a.n << (a.nlev - 1)) : a.n;
+  const size_t lds = (size_t)htop * C * sizeof(double);
+  if (hipError_t e = prep(k, lds)) return e;
+  const dim3 grid((unsigned)(a.nouter * ncb(a.inner, C)));
+  hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.sv, a.dst, a.dv, a.n, a.nlev, a.inner,
+                     rev_taps<L>(b));
+  return hipGetLastError();
+}
+template <int L, int C>
+hipError_t fwt_fwd_tile_go(const Bank& b, const TileArgs& a, hipStream_t s) {
+  constexpr int T = fwt_T<C>(), KM = fwt_K<C>();
+  auto k = fwt_fwd_tile<L, C, NT, T, KM, kFMA>;
+  const int m0 = T + (b.L - 2) * ((1 << a.K) - 1);
+  const size_t lds = (size_t)m0 * C * sizeof(double);
+  if (hipError_t e = prep(k, lds)) return e;
+  const dim3 grid((unsigned)(a.nouter * ncb(a.inner, C) * (a.h / T)));
+  hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.sv, a.dst, a.dv, a.adst, a.av, a.h, a.K,
+                     a.inner, fwd_taps<L>(b));
+  return hipGetLastError();
+}
+template <int L, int C>
+hipError_t fwt_rev_tile_go(const Bank& b, const TileArgs& a, hipStream_t s) {
+  constexpr int T = fwt_T<C>(), KM = fwt_K<C>();
+  constexpr int QM = (LMax<L>::v + 1) / 2;
+  auto k = fwt_rev_tile<L, C, NT, T, KM, kFMA>;
+  const size_t lds = (size_t)2 * (T / 2 + 2 * QM + 4) * C * sizeof(double);
+  if (hipError_t e = prep(k, lds)) return e;
+  const int hK = a.h << (a.K - 1);
+  const dim3 grid((unsigned)(a.nouter * ncb(a.inner, C) * (hK / T)));
+  hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.sv, a.coef, a.cv, a.dst, a.dv, a.h, a.K,
+                     a.inner, rev_taps<L>(b));
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------- WPT
+template <int L, int C>
+hipError_t wpt_fwd_res_go(const Bank& b, const ResArgs& a, hipStream_t s) {
+  auto k = wpt_fwd_res<L, C, NT, cap<C>(), kFMA>;
+  const size_t lds = (size_t)a.n * C * sizeof(double);
+  if (hipError_t e = prep(k, lds)) return e;
+  const dim3 grid((unsigned)(a.nouter * ncb(a.inner, C)));
+  hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.sv, a.dst, a.dv, a.n, a.nlev, a.inner,
+                     fwd_taps<L>(b));
+  return hipGetLastError();
+}
+template <int L, int C>
+hipError_t wpt_rev_res_go(const Bank& b, const ResArgs& a, hipStream_t s) {
+  auto k = wpt_rev_res<L, C, NT, cap<C>(), kFMA>;
+  const size_t lds = (size_t)a.n * C * sizeof(double);
+  if (hipError_t e = prep(k, lds)) return e;
+  const dim3 grid((unsigned)(a.nouter * ncb(a.inner, C)));
+  hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.sv, a.dst, a.dv, a.n, a.h0, a.nlev,
+                     a.inner, rev_taps<L>(b));
+  return hipGetLastError();
+}
+template <int L, int C>
+hipError_t wpt_fwd_tile_go(const Bank& b, const TileArgs& a, hipStream_t s) {
+  constexpr int T = wpt_T<C>(), KM = wpt_K<C>();
+  auto k = wpt_fwd_tile<L, C, NT, T, KM, kFMA>;
+  const int m0 = T + (b.L - 2) * ((1 << a.K) - 1);
+  const size_t lds = (size_t)m0 * C * sizeof(double);
+  if (hipError_t e = prep(k, lds)) return e;
+  const dim3 grid((unsigned)(a.nouter * ncb(a.inner, C) * (a.h / T)));
+  hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.sv, a.dst, a.dv, a.h, a.K, a.inner,
+                     fwd_taps<L>(b));
+  return hipGetLastError();
+}
+template <int L, int C>
+hipError_t wpt_rev_tile_go(const Bank& b, const TileArgs& a, hipStream_t s) {
+  constexpr int T = wpt_T<C>(), KM = wpt_K<C>();
+  constexpr int QM = (LMax<L>::v + 1) / 2;
+  auto k = wpt_rev_tile<L, C, NT, T, KM, kFMA>;
+  const size_t lds = (size_t)(T + (1 << KM) * (2 * QM + 4)) * C * sizeof(double);
+  if (hipError_t e = prep(k, lds)) return e;
+  const dim3 grid((unsigned)(a.nouter * ncb(a.inner, C) * (a.h / T)));
+  hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.sv, a.dst, a.dv, a.h, a.K, a.inner,
+                     rev_taps<L>(b));
+  return hipGetLastError();
+}
+
+}  // namespace
+
+// L dispatch: compiled-in tap counts, else the runtime-L kernels.  A scaled
+// synthesis bank (Haar1Orthogonal) always takes the runtime-L reverse path.
+#define JWV_DISPATCH(GO, b, C, a, s, rev)                                   \
+  do {                                                                      \
+    const int L_ = ((rev) && (b).scale != 1.0) ? 0 : static_l((b).L);       \
+    if ((C) == 1) {                                                         \
+      switch (L_) {                                                         \
+        case 2: return GO<2, 1>(b, a, s);                                   \
+        case 4: return GO<4, 1>(b, a, s);                                   \
+        case 8: return GO<8, 1>(b, a, s);                                   \
+        case 16: return GO<16, 1>(b, a, s);                                 \
+        default: return GO<0, 1>(b, a, s);                                  \
+      }                                                                     \
+    }                                                                       \
+    switch (L_) {                                                           \
+      case 2: return GO<2, 8>(b, a, s);                                     \
+      case 4: return GO<4, 8>(b, a, s);                                     \
+      case 8: return GO<8, 8>(b, a, s);                                     \
+      case 16: return GO<16, 8>(b, a, s);                                   \
+      default: return GO<0, 8>(b, a, s);                                    \
+    }                                                                       \
+  } while (0)
+
+namespace JWV_NS {
+hipError_t fwt_fwd_res(const Bank& b, int C, const ResArgs& a, hipStream_t s) {
+  JWV_DISPATCH(fwt_fwd_res_go, b, C, a, s, false);
+}
+hipError_t fwt_rev_res(const Bank& b, int C, const ResArgs& a, hipStream_t s) {
+  JWV_DISPATCH(fwt_rev_res_go, b, C, a, s, true);
+}
+hipError_t fwt_fwd_tile(const Bank& b, int C, const TileArgs& a, hipStream_t s) {
+  JWV_DISPATCH(fwt_fwd_tile_go, b, C, a, s, false);
+}
+hipError_t fwt_rev_tile(const Bank& b, int C, const TileArgs& a, hipStream_t s) {
+  JWV_DISPATCH(fwt_rev_tile_go, b, C, a, s, true);
+}
+hipError_t wpt_fwd_res(const Bank& b, int C, const ResArgs& a, hipStream_t s) {
+  JWV_DISPATCH(wpt_fwd_res_go, b, C, a, s, false);
+}
+hipError_t wpt_rev_res(const Bank& b, int C, const ResArgs& a, hipStream_t s) {
+  JWV_DISPATCH(wpt_rev_res_go, b, C, a, s, true);
+}
+hipError_t wpt_fwd_tile(const Bank& b, int C, const TileArgs& a, hipStream_t s) {
+  JWV_DISPATCH(wpt_fwd_tile_go, b, C, a, s, false);
+}
+hipError_t wpt_rev_tile(const Bank& b, int C, const TileArgs& a, hipStream_t s) {
+  JWV_DISPATCH(wpt_rev_tile_go, b, C, a, s, true);
+}
+}  // namespace JWV_NS
+
+}  // namespace jwv

@@ -1,0 +1,539 @@
+"""Host mirror of JWave's operator surface over libjwave_hip.so.
+
+Same names, argument meaning and error behaviour as the reference classes:
+  Transform (facade)            jwave/Transform.java:43-512
+  BasicTransform (operator SPI) jwave/transforms/BasicTransform.java:42-699
+  WaveletTransform              jwave/transforms/WaveletTransform.java:34-183
+  FastWaveletTransform          jwave/transforms/FastWaveletTransform.java:39-154
+  WaveletPacketTransform        jwave/transforms/WaveletPacketTransform.java:40-193
+  MODWTTransform                jwave/transforms/MODWTTransform.java:104-913
+Validation happens here first, with the reference's exception types and
+messages (as the JNI shim does); every transform then runs on the
+GPU through the C ABI.  There is no CPU compute path.
+
+Arrays: numpy float64 arrays use the host-pointer entry points (copy in,
+compute, copy out).  torch float64 CUDA tensors use the ``_dev`` entry points
+on torch's current stream (no host round trip).
+"""
+import ctypes
+import threading
+
+import numpy as np
+
+from . import _lib as L
+from .exceptions import JWaveError, JWaveException, JWaveFailure
+from .wavelets import Wavelet
+
+MAX_DECOMPOSITION_LEVEL = 13  # MODWTTransform.java:111
+
+_BINARY_MSG = ("given array length is not 2^p | p E N ... = 1, 2, 4, 8, 16, 32, .. "
+               "please use the Ancient Egyptian Decomposition for any other array length!")
+
+
+def is_binary(n):
+    """MathToolKit.isBinary (tools/MathToolKit.java:185-188)."""
+    n = int(n)
+    return n > 0 and (n & (n - 1)) == 0
+
+
+def get_exponent(n):
+    """MathToolKit.getExponent for powers of two (tools/MathToolKit.java:202-206)."""
+    n = int(n)
+    return n.bit_length() - 1 if n > 0 else 0
+
+
+# ----------------------------------------------------------------- context
+class Context:
+    """A jwv_ctx: one device, one stream, a math mode ("exact" | "fma")."""
+
+    def __init__(self, device=0, math="exact"):
+        self._lib = L.lib()
+        h = ctypes.c_void_p()
+        rc = self._lib.jwv_ctx_create(int(device), ctypes.byref(h))
+        if rc != 0:
+            raise JWaveError(self._lib.jwv_last_error(None).decode())
+        self.handle = h
+        self.device = int(device)
+        self.set_math(math)
+
+    def set_math(self, math):
+        mode = {"exact": L.JWV_MATH_EXACT, "fma": L.JWV_MATH_FMA}[math]
+        self._check(self._lib.jwv_ctx_set_math(self.handle, mode))
+        self.math = math
+
+    def set_stream(self, stream_handle):
+        self._check(self._lib.jwv_ctx_set_stream(self.handle, stream_handle))
+
+    def synchronize(self):
+        self._check(self._lib.jwv_ctx_synchronize(self.handle))
+
+    def profile(self, on=True):
+        """Record hipEvents around every kernel launch (see jwv_ctx_profile_enable)."""
+        self._check(self._lib.jwv_ctx_profile_enable(self.handle, 1 if on else 0))
+
+    def profile_read(self):
+        """-> {kind: {"launches", "total_ms", "bytes"}} since the last read (synchronises)."""
+        arr = (L.KernelStat * 32)()
+        n = ctypes.c_int(0)
+        self._check(self._lib.jwv_ctx_profile_read(self.handle, arr, 32, ctypes.byref(n)))
+        return {arr[i].name.decode(): {"launches": int(arr[i].launches),
+                                       "total_ms": float(arr[i].total_ms),
+                                       "bytes": float(arr[i].bytes)} for i in range(n.value)}
+
+    def trim(self):
+        self._check(self._lib.jwv_ctx_trim(self.handle))
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self._lib.jwv_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc == 0:
+            return
+        msg = (self._lib.jwv_last_error(self.handle) or b"").decode()
+        if rc == L.JWV_ERR_FAILURE:
+            raise JWaveFailure(msg)
+        if rc == L.JWV_ERR_ILLEGAL_ARGUMENT:
+            raise ValueError(msg)  # IllegalArgumentException
+        raise JWaveError(msg)
+
+
+_tls = threading.local()
+
+
+def default_context(device=0):
+    ctxs = getattr(_tls, "ctxs", None)
+    if ctxs is None:
+        ctxs = _tls.ctxs = {}
+    if device not in ctxs:
+        ctxs[device] = Context(device)
+    return ctxs[device]
+
+
+class _TapsHolder:
+    """Keeps numpy tap arrays alive next to the jwv_taps struct."""
+    _cache = {}
+
+    def __init__(self, w):
+        dp = ctypes.POINTER(ctypes.c_double)
+        self.arrs = [np.ascontiguousarray(np.asarray(v, dtype=np.float64))
+                     for v in (w.lo, w.hi, w.lo_r, w.hi_r)]
+        self.s = L.Taps(w.mother_wavelength, w.transform_wavelength,
+                        *[a.ctypes.data_as(dp) for a in self.arrs], w.reverse_scale)
+
+    @classmethod
+    def of(cls, w):
+        key = id(w)
+        ent = cls._cache.get(key)
+        if ent is None or ent[0] is not w:
+            ent = (w, cls(w))
+            cls._cache[key] = ent
+        return ctypes.byref(ent[1].s)
+
+
+def _is_torch(x):
+    return type(x).__module__.startswith("torch")
+
+
+def _prep(x, ctx):
+    """-> (ptr, keepalive, is_device, like) for an input array."""
+    if _is_torch(x):
+        import torch
+        if not x.is_cuda:
+            x = x.detach().numpy()
+        else:
+            if x.dtype != torch.float64:
+                raise JWaveFailure("device arrays must be float64")
+            x = x.contiguous()
+            ctx.set_stream(torch.cuda.current_stream(x.device).cuda_stream)
+            return ctypes.c_void_p(x.data_ptr()), x, True
+    a = np.ascontiguousarray(np.asarray(x, dtype=np.float64))
+    return ctypes.c_void_p(a.ctypes.data), a, False
+
+
+def _empty(like, shape, dev):
+    if dev:
+        import torch
+        return torch.empty(shape, dtype=torch.float64, device=like.device)
+    return np.empty(shape, dtype=np.float64)
+
+
+def _ptr(out, dev):
+    return ctypes.c_void_p(out.data_ptr() if dev else out.ctypes.data)
+
+
+# --------------------------------------------------------- functional layer
+def _run(fn_host, fn_dev, ctx, x, out_shape, args):
+    ctx = ctx or default_context()
+    px, keep, dev = _prep(x, ctx)
+    out = _empty(keep, out_shape, dev)
+    lib = L.lib()
+    fn = getattr(lib, fn_dev if dev else fn_host)
+    ctx._check(fn(px, _ptr(out, dev), *args, ctx.handle))
+    return out
+
+
+def fwt_forward(x, wavelet, level, ctx=None, kind="fwt"):
+    """Forward FWT/WPT of one signal (1-D) or a batch of signals (2-D array, one per row)."""
+    shape = tuple(x.shape)
+    t = _TapsHolder.of(wavelet)
+    if len(shape) == 1:
+        return _run("jwv_%s_fwd_f64" % kind, "jwv_%s_fwd_f64_dev" % kind, ctx, x, shape,
+                    (shape[0], int(level), t))
+    b, n = shape
+    return _run("jwv_%s_fwd_batch_f64" % kind, "jwv_%s_fwd_batch_f64_dev" % kind, ctx, x, shape,
+                (b, n, n, int(level), t))
+
+
+def fwt_reverse(y, wavelet, level, ctx=None, kind="fwt"):
+    shape = tuple(y.shape)
+    t = _TapsHolder.of(wavelet)
+    if len(shape) == 1:
+        return _run("jwv_%s_rev_f64" % kind, "jwv_%s_rev_f64_dev" % kind, ctx, y, shape,
+                    (shape[0], int(level), t))
+    b, n = shape
+    return _run("jwv_%s_rev_batch_f64" % kind, "jwv_%s_rev_batch_f64_dev" % kind, ctx, y, shape,
+                (b, n, n, int(level), t))
+
+
+def wpt_forward(x, wavelet, level, ctx=None):
+    return fwt_forward(x, wavelet, level, ctx, kind="wpt")
+
+
+def wpt_reverse(y, wavelet, level, ctx=None):
+    return fwt_reverse(y, wavelet, level, ctx, kind="wpt")
+
+
+def transform_2d(x, wavelet, lvl_m, lvl_n, forward=True, ctx=None, kind="fwt"):
+    r, c = x.shape
+    d = "fwd" if forward else "rev"
+    return _run("jwv_%s2d_%s_f64" % (kind, d), "jwv_%s2d_%s_f64_dev" % (kind, d), ctx, x,
+                (r, c), (r, c, int(lvl_m), int(lvl_n), _TapsHolder.of(wavelet)))
+
+
+def transform_3d(x, wavelet, lvl_p, lvl_q, lvl_r, forward=True, ctx=None, kind="fwt"):
+    p, q, r = x.shape
+    d = "fwd" if forward else "rev"
+    dev_name = "jwv_%s3d_%s_f64_dev" % (kind, d) if kind == "fwt" else None
+    if _is_torch(x) and getattr(x, "is_cuda", False) and dev_name is None:
+        raise JWaveError("device 3-D packet transform is not exported")
+    return _run("jwv_%s3d_%s_f64" % (kind, d), dev_name, ctx, x, (p, q, r),
+                (p, q, r, int(lvl_p), int(lvl_q), int(lvl_r), _TapsHolder.of(wavelet)))
+
+
+def modwt_forward(x, wavelet, J, ctx=None):
+    n = x.shape[0]
+    return _run("jwv_modwt_fwd_f64", "jwv_modwt_fwd_f64_dev", ctx, x, (int(J) + 1, n),
+                (n, int(J), _TapsHolder.of(wavelet)))
+
+
+def modwt_inverse(coeffs, wavelet, ctx=None):
+    J = coeffs.shape[0] - 1
+    n = coeffs.shape[1]
+    return _run("jwv_modwt_inv_f64", "jwv_modwt_inv_f64_dev", ctx, coeffs, (n,),
+                (n, int(J), _TapsHolder.of(wavelet)))
+
+
+def modwt_filters(wavelet):
+    g = np.empty(wavelet.mother_wavelength)
+    h = np.empty(wavelet.mother_wavelength)
+    dp = ctypes.POINTER(ctypes.c_double)
+    rc = L.lib().jwv_modwt_filters(_TapsHolder.of(wavelet), g.ctypes.data_as(dp),
+                                   h.ctypes.data_as(dp))
+    if rc:
+        raise JWaveError(L.lib().jwv_last_error(None).decode())
+    return g, h
+
+
+# ------------------------------------------------------ operator-class mirror
+class BasicTransform:
+    """jwave.transforms.BasicTransform (BasicTransform.java:42): 1-D/2-D/3-D
+    forward/reverse overloads dispatch on the array rank."""
+
+    kind = None  # "fwt" | "wpt"
+
+    def __init__(self, wavelet=None, ctx=None):
+        self._wavelet = wavelet
+        self._ctx = ctx
+        self._name = None
+
+    def getName(self):  # noqa: N802
+        return self._name
+
+    def getWavelet(self):  # noqa: N802
+        if self._wavelet is None:
+            raise JWaveFailure("BasicTransform#getWavelet - not available")
+        return self._wavelet
+
+    # -- overload dispatch --------------------------------------------------
+    def forward(self, a, *levels):
+        nd = len(np.shape(a)) if not _is_torch(a) else a.dim()
+        if nd == 1:
+            return self.forward_1d(a, *levels)
+        if nd == 2:
+            return self.forward_2d(a, *levels)
+        if nd == 3:
+            return self.forward_3d(a, *levels)
+        raise JWaveFailure("unsupported array rank %d" % nd)
+
+    def reverse(self, a, *levels):
+        nd = len(np.shape(a)) if not _is_torch(a) else a.dim()
+        if nd == 1:
+            return self.reverse_1d(a, *levels)
+        if nd == 2:
+            return self.reverse_2d(a, *levels)
+        if nd == 3:
+            return self.reverse_3d(a, *levels)
+        raise JWaveFailure("unsupported array rank %d" % nd)
+
+    # -- 2-D: BasicTransform.java:336-474 ----------------------------------
+    def forward_2d(self, m, lvl_m=None, lvl_n=None):
+        r, c = m.shape
+        if lvl_m is None:
+            lvl_m, lvl_n = get_exponent(r), get_exponent(c)
+        self._check_1d(c, lvl_n, True)
+        self._check_1d(r, lvl_m, True)
+        return transform_2d(m, self._wavelet, lvl_m, lvl_n, True, self._ctx, self.kind)
+
+    def reverse_2d(self, m, lvl_m=None, lvl_n=None):
+        r, c = m.shape
+        if lvl_m is None:
+            lvl_m, lvl_n = get_exponent(r), get_exponent(c)
+        self._check_1d(r, lvl_m, False)
+        self._check_1d(c, lvl_n, False)
+        return transform_2d(m, self._wavelet, lvl_m, lvl_n, False, self._ctx, self.kind)
+
+    # -- 3-D: BasicTransform.java:487-659 ----------------------------------
+    def forward_3d(self, s, lvl_p=None, lvl_q=None, lvl_r=None):
+        p, q, r = s.shape
+        if lvl_p is None:
+            lvl_p, lvl_q, lvl_r = get_exponent(p), get_exponent(q), get_exponent(r)
+        self._check_1d(r, lvl_q, True)
+        self._check_1d(q, lvl_p, True)
+        self._check_1d(p, lvl_r, True)
+        return transform_3d(s, self._wavelet, lvl_p, lvl_q, lvl_r, True, self._ctx, self.kind)
+
+    def reverse_3d(self, s, lvl_p=None, lvl_q=None, lvl_r=None):
+        p, q, r = s.shape
+        if lvl_p is None:
+            lvl_p, lvl_q, lvl_r = get_exponent(p), get_exponent(q), get_exponent(r)
+        self._check_1d(q, lvl_p, False)
+        self._check_1d(r, lvl_q, False)
+        self._check_1d(p, lvl_r, False)
+        return transform_3d(s, self._wavelet, lvl_p, lvl_q, lvl_r, False, self._ctx, self.kind)
+
+    def _check_1d(self, n, level, fwd):
+        raise NotImplementedError
+
+
+class WaveletTransform(BasicTransform):
+    """jwave.transforms.WaveletTransform (WaveletTransform.java:34-183)."""
+
+    _who = "WaveletTransform"
+
+    def forward_1d(self, arr, level=None):
+        n = arr.shape[0]
+        if level is None:  # WaveletTransform.forward(double[]) :77-88
+            if not is_binary(n):
+                raise JWaveFailure("WaveletTransform#forward - " + _BINARY_MSG)
+            level = get_exponent(n)
+        self._check_1d(n, level, True)
+        return fwt_forward(arr, self._wavelet, level, self._ctx, self.kind)
+
+    def reverse_1d(self, arr, level=None):
+        n = arr.shape[0]
+        if level is None:  # :101-112
+            if not is_binary(n):
+                raise JWaveFailure("WaveletTransform#reverse - " + _BINARY_MSG)
+            level = get_exponent(n)
+        self._check_1d(n, level, False)
+        return fwt_reverse(arr, self._wavelet, level, self._ctx, self.kind)
+
+    def forward_batch(self, signals, level=None):
+        """Batched 1-D forward: one row per independent signal (one native call)."""
+        n = signals.shape[1]
+        level = get_exponent(n) if level is None else level
+        self._check_1d(n, level, True)
+        return fwt_forward(signals, self._wavelet, level, self._ctx, self.kind)
+
+    def reverse_batch(self, coeffs, level=None):
+        n = coeffs.shape[1]
+        level = get_exponent(n) if level is None else level
+        self._check_1d(n, level, False)
+        return fwt_reverse(coeffs, self._wavelet, level, self._ctx, self.kind)
+
+    # WaveletTransform.decompose / recompose (:136-182)
+    def decompose(self, arr):
+        n = arr.shape[0]
+        levels = get_exponent(n)
+        return np.stack([np.asarray(self.forward_1d(arr, p)) for p in range(levels + 1)])
+
+    def recompose(self, mat, level=None):
+        if level is None:
+            level = len(mat) - 1
+        if level < 0 or level >= len(mat):
+            raise JWaveFailure("WaveletTransform#recompose - given level is out of range")
+        return self.reverse_1d(np.asarray(mat[level]), level)
+
+
+class FastWaveletTransform(WaveletTransform):
+    """FastWaveletTransform.java:39-154 — Mallat pyramid on the GPU."""
+
+    kind = "fwt"
+
+    def __init__(self, wavelet, ctx=None):
+        super().__init__(wavelet, ctx)
+        self._name = "Fast Wavelet Transform"
+
+    def _check_1d(self, n, level, fwd):
+        who = "FastWaveletTransform#%s - " % ("forward" if fwd else "reverse")
+        if not is_binary(n):  # :74-78 / :122-126
+            raise JWaveFailure(who + _BINARY_MSG)
+        if level < 0 or level > get_exponent(n):  # :80-83 / :128-131
+            raise JWaveFailure(who + "given level is out of range for given array")
+
+
+class WaveletPacketTransform(WaveletTransform):
+    """WaveletPacketTransform.java:40-193 — full packet tree on the GPU."""
+
+    kind = "wpt"
+
+    def __init__(self, wavelet, ctx=None):
+        super().__init__(wavelet, ctx)
+        self._name = "Wavelet Packet Transform"
+
+    def _check_1d(self, n, level, fwd):
+        if not is_binary(n):  # :76-79
+            raise JWaveFailure(_BINARY_MSG)
+        if level < 0 or level > get_exponent(n):  # :81-84
+            raise JWaveFailure("WaveletPacketTransform#%s - given level is out of range for given"
+                               " array" % ("forward" if fwd else "reverse"))
+
+
+class PooledWaveletPacketTransform(WaveletPacketTransform):
+    """PooledWaveletPacketTransform.java:24-127: same math; forward rejects level 0 (:29)."""
+
+    def _check_1d(self, n, level, fwd):
+        if fwd:
+            if not is_binary(n):
+                raise JWaveFailure("PooledWaveletPacketTransform#forward - array length is not 2^p")
+            if level <= 0 or level > get_exponent(n):
+                raise JWaveFailure("PooledWaveletPacketTransform#forward - invalid level")
+            return
+        super()._check_1d(n, level, fwd)
+
+
+class ParallelWaveletPacketTransform(WaveletPacketTransform):
+    """ParallelWaveletPacketTransform.java: same math as the sequential WPT."""
+
+
+class MODWTTransform(WaveletTransform):
+    """MODWTTransform.java:104-913 (DIRECT convolution semantics)."""
+
+    kind = None
+
+    def __init__(self, wavelet, ctx=None):
+        super().__init__(wavelet, ctx)
+        self._name = "MODWT"
+
+    @staticmethod
+    def getMaxDecompositionLevel():  # noqa: N802
+        return MAX_DECOMPOSITION_LEVEL
+
+    def forwardMODWT(self, data, maxLevel):  # noqa: N802,N803 — :256-306
+        if maxLevel < 1:
+            raise ValueError("MODWTTransform#forwardMODWT - decomposition level must be at least 1,"
+                             " requested: %d" % maxLevel)
+        if maxLevel > MAX_DECOMPOSITION_LEVEL:
+            raise ValueError("MODWTTransform#forwardMODWT - maximum supported decomposition level"
+                             " is %d, requested: %d" % (MAX_DECOMPOSITION_LEVEL, maxLevel))
+        if data is None or len(data) == 0:
+            return np.zeros((maxLevel + 1, 0))
+        n = len(data)
+        theo = n.bit_length() - 1
+        if maxLevel > theo:
+            raise ValueError("Decomposition level %d exceeds theoretical limit %d for signal length"
+                             " %d" % (maxLevel, theo, n))
+        return modwt_forward(data, self._wavelet, maxLevel, self._ctx)
+
+    def inverseMODWT(self, coefficients):  # noqa: N802 — :337-375
+        if coefficients is None or len(coefficients) <= 1:
+            return np.zeros(0)
+        if _is_torch(coefficients):
+            return modwt_inverse(coefficients, self._wavelet, self._ctx)
+        c = np.ascontiguousarray(np.asarray(coefficients, dtype=np.float64))
+        return modwt_inverse(c, self._wavelet, self._ctx)
+
+    # flattened pow-2 API (:389-443)
+    def forward_1d(self, arr, level=None):
+        n = len(arr)
+        if n == 0:
+            return np.zeros(0)
+        if not is_binary(n):
+            raise JWaveFailure("MODWTTransform#forward - given array length is not 2^p | p E N"
+                               " ... = 1, 2, 4, 8, 16, 32, .. ")
+        if level is None:
+            level = get_exponent(n)
+        if level < 0 or level > get_exponent(n):
+            raise JWaveFailure("MODWTTransform#forward - given level is out of range for given"
+                               " array")
+        if level > MAX_DECOMPOSITION_LEVEL:
+            raise JWaveFailure("MODWTTransform#forward - maximum supported decomposition level is"
+                               " %d, requested: %d" % (MAX_DECOMPOSITION_LEVEL, level))
+        return np.asarray(self.forwardMODWT(arr, level)).reshape(-1)
+
+    def reverse_1d(self, arr, level=None):
+        if len(arr) == 0:
+            return np.zeros(0)
+        n = len(arr) // (level + 1)
+        if not is_binary(n):
+            raise JWaveFailure("MODWTTransform#reverse - Invalid coefficient array for given level")
+        if len(arr) != n * (level + 1):
+            raise JWaveFailure("MODWTTransform#reverse - Coefficient array length does not match"
+                               " expected size for given level")
+        return self.inverseMODWT(np.asarray(arr).reshape(level + 1, n))
+
+    def _check_1d(self, n, level, fwd):
+        pass
+
+
+class Transform:
+    """Final facade (Transform.java:43-512): delegates to a BasicTransform and,
+    like the reference (:81-90), prints a JWaveException and returns None."""
+
+    def __init__(self, transform):
+        if transform is None:
+            raise JWaveFailure("Transform - no transform given")
+        self._transform = transform
+
+    def _safe(self, fn, *a):
+        try:
+            return fn(*a)
+        except JWaveException as e:
+            print("%s: %s" % (type(e).__name__, e.getMessage()))
+            return None
+
+    def forward(self, a, *levels):
+        return self._safe(self._transform.forward, a, *levels)
+
+    def reverse(self, a, *levels):
+        return self._safe(self._transform.reverse, a, *levels)
+
+    def decompose(self, a):
+        return self._safe(self._transform.decompose, a)
+
+    def recompose(self, m, level=None):
+        return self._safe(self._transform.recompose, m, level)
+
+    def getWavelet(self):  # noqa: N802
+        return self._safe(self._transform.getWavelet)
+
+    def getBasicTransform(self):  # noqa: N802
+        return self._transform

@@ -1,0 +1,317 @@
+"""GPU parity: libjwave_hip.so (through the C ABI) vs the CPU oracle.
+
+Bar: EXACT math is bit-identical to the oracle (which evaluates the Java loops
+in the Java order without FMA).  FMA math: |diff| <= 1e-12 * max(1, max|ref|)
+(BASELINE.md parity gates).  Round trips are additionally compared with the
+input.  Sizes cover both kernel shapes (resident <= 8192 per signal, tiled
+above), wrap-around at every level, tiny levels (h < L), odd / long / scaled
+banks and non power-of-two MODWT lengths.
+"""
+import numpy as np
+import pytest
+
+import oracle
+import jwave_amd as jw
+from jwave_amd import transforms as T
+
+pytestmark = pytest.mark.gpu
+
+FMA_TOL = 1e-12
+
+# config wavelets + the generic-kernel cases (odd L, long L, scaled, tw=8, biorthogonal)
+WAVELETS = ["Haar1", "Daubechies2", "Daubechies4", "Daubechies8", "Symlet8", "Coiflet1",
+            "Daubechies20", "Haar1Orthogonal", "BiOrthogonal13", "BiOrthogonal35", "CDF53",
+            "Battle23", "DiscreteMeyer", "Legendre3", "Symlet2"]
+
+
+def rnd(n, seed=42):
+    return oracle.java_random_doubles(seed, n)
+
+
+def assert_exact(got, ref, what=""):
+    got = np.asarray(got)
+    if not np.array_equal(got, ref):
+        d = np.abs(got - ref)
+        i = int(np.argmax(d))
+        raise AssertionError("%s not bit-exact: max|diff|=%g at %d (got %r ref %r)"
+                             % (what, d.max(), i, got.flat[i], ref.flat[i]))
+
+
+def assert_close(got, ref, what=""):
+    got = np.asarray(got)
+    tol = FMA_TOL * max(1.0, float(np.abs(ref).max()) if ref.size else 1.0)
+    d = float(np.abs(got - ref).max()) if ref.size else 0.0
+    assert d <= tol, "%s: max|diff| %g > %g" % (what, d, tol)
+
+
+def levels_for(n, w):
+    full = int(n).bit_length() - 1
+    return sorted({0, 1, full // 2, full})
+
+
+# ------------------------------------------------------------------ 1-D FWT
+@pytest.mark.parametrize("wname", WAVELETS)
+def test_fwt_small_all_levels(ctx, wname):
+    w = jw.by_class(wname)
+    for n in (1, 2, 4, 8, 16, 32, 64, 256, 1024):
+        x = rnd(n, 7 + n)
+        for lev in range(0, int(n).bit_length()):
+            y = T.fwt_forward(x, w, lev, ctx)
+            assert_exact(y, oracle.fwt_forward(w, x, lev), "%s fwd n=%d l=%d" % (wname, n, lev))
+            xr = T.fwt_reverse(y, w, lev, ctx)
+            assert_exact(xr, oracle.fwt_reverse(w, np.asarray(y), lev),
+                         "%s rev n=%d l=%d" % (wname, n, lev))
+
+
+@pytest.mark.parametrize("wname", WAVELETS)
+@pytest.mark.parametrize("n", [8192, 16384, 1 << 16, 1 << 18])
+def test_fwt_large(ctx, wname, n):
+    w = jw.by_class(wname)
+    x = rnd(n, n)
+    for lev in levels_for(n, w):
+        y = T.fwt_forward(x, w, lev, ctx)
+        yr = oracle.fwt_forward(w, x, lev)
+        assert_exact(y, yr, "%s fwd n=%d l=%d" % (wname, n, lev))
+        xr = T.fwt_reverse(yr, w, lev, ctx)
+        assert_exact(xr, oracle.fwt_reverse(w, yr, lev), "%s rev n=%d l=%d" % (wname, n, lev))
+
+
+@pytest.mark.parametrize("wname", ["Haar1", "Daubechies4", "Daubechies8", "Symlet8", "Coiflet1"])
+def test_fwt_fma_mode(ctx_fma, wname):
+    w = jw.by_class(wname)
+    for n in (64, 4096, 1 << 15, 1 << 17):
+        x = rnd(n, 3)
+        lev = int(n).bit_length() - 1
+        yr = oracle.fwt_forward(w, x, lev)
+        assert_close(T.fwt_forward(x, w, lev, ctx_fma), yr, "fma fwd %s %d" % (wname, n))
+        assert_close(T.fwt_reverse(yr, w, lev, ctx_fma), oracle.fwt_reverse(w, yr, lev),
+                     "fma rev %s %d" % (wname, n))
+
+
+@pytest.mark.parametrize("wname", ["Haar1", "Daubechies4", "Symlet8", "Coiflet1"])
+def test_fwt_batch(ctx, wname):
+    w = jw.by_class(wname)
+    for b, n in ((5, 64), (3, 8192), (2, 32768)):
+        x = np.stack([rnd(n, 100 + i) for i in range(b)])
+        for lev in (1, int(n).bit_length() - 1):
+            y = T.fwt_forward(x, w, lev, ctx)
+            yr = oracle.batch("fwt", True, w, x, lev)
+            assert_exact(y, yr, "batch fwd")
+            assert_exact(T.fwt_reverse(yr, w, lev, ctx), oracle.batch("fwt", False, w, yr, lev),
+                         "batch rev")
+
+
+def test_fwt_config2_full_size(ctx):
+    """Config 2: Daubechies4, N = 2^24, full depth — exact vs oracle, and the
+    round trip vs the input (reported bound from the taps' precision)."""
+    w = jw.by_class("Daubechies4")
+    n = 1 << 24
+    x = rnd(n, 42)
+    y = T.fwt_forward(x, w, 24, ctx)
+    yr = oracle.fwt_forward(w, x, 24)
+    assert_exact(y, yr, "D4 2^24 fwd")
+    xr = T.fwt_reverse(y, w, 24, ctx)
+    assert_exact(xr, oracle.fwt_reverse(w, yr, 24), "D4 2^24 rev")
+    assert np.abs(xr - x).max() < 1e-11
+
+
+# ------------------------------------------------------------------ WPT
+@pytest.mark.parametrize("wname", WAVELETS)
+def test_wpt_small(ctx, wname):
+    w = jw.by_class(wname)
+    for n in (2, 4, 16, 64, 1024, 8192):
+        x = rnd(n, 11 + n)
+        for lev in levels_for(n, w):
+            y = T.wpt_forward(x, w, lev, ctx)
+            yr = oracle.wpt_forward(w, x, lev)
+            assert_exact(y, yr, "%s wpt fwd n=%d l=%d" % (wname, n, lev))
+            assert_exact(T.wpt_reverse(yr, w, lev, ctx), oracle.wpt_reverse(w, yr, lev),
+                         "%s wpt rev n=%d l=%d" % (wname, n, lev))
+
+
+@pytest.mark.parametrize("wname", ["Haar1", "Daubechies4", "Symlet8", "Coiflet1", "Battle23"])
+@pytest.mark.parametrize("n", [16384, 1 << 16, 1 << 17])
+def test_wpt_large(ctx, wname, n):
+    w = jw.by_class(wname)
+    x = rnd(n, 5)
+    full = int(n).bit_length() - 1
+    for lev in (1, 6, 8, full):
+        y = T.wpt_forward(x, w, lev, ctx)
+        yr = oracle.wpt_forward(w, x, lev)
+        assert_exact(y, yr, "%s wpt fwd n=%d l=%d" % (wname, n, lev))
+        assert_exact(T.wpt_reverse(yr, w, lev, ctx), oracle.wpt_reverse(w, yr, lev),
+                     "%s wpt rev n=%d l=%d" % (wname, n, lev))
+
+
+def test_wpt_config4_shape(ctx, ctx_fma):
+    """Config 4 shape (Symlet8, 6 levels, N=65536) on a small batch; FMA too."""
+    w = jw.by_class("Symlet8")
+    x = np.stack([rnd(1 << 16, 42 + i) for i in range(4)])
+    yr = oracle.batch("wpt", True, w, x, 6)
+    assert_exact(T.wpt_forward(x, w, 6, ctx), yr, "wpt cfg4 fwd")
+    xr_ref = oracle.batch("wpt", False, w, yr, 6)
+    assert_exact(T.wpt_reverse(yr, w, 6, ctx), xr_ref, "wpt cfg4 rev")
+    assert_close(T.wpt_forward(x, w, 6, ctx_fma), yr, "wpt cfg4 fwd fma")
+    assert_close(T.wpt_reverse(yr, w, 6, ctx_fma), xr_ref, "wpt cfg4 rev fma")
+
+
+# ------------------------------------------------------------------ 2-D / 3-D
+@pytest.mark.parametrize("wname", ["Haar1", "Daubechies4", "Daubechies8", "Coiflet1", "Battle23"])
+@pytest.mark.parametrize("shape", [(2, 2), (8, 4), (64, 64), (256, 32), (32, 256), (2048, 16),
+                                   (16, 16384), (4096, 64)])
+def test_fwt2d(ctx, wname, shape):
+    w = jw.by_class(wname)
+    r, c = shape
+    x = rnd(r * c, r + c).reshape(r, c)
+    for lm, ln in ((r.bit_length() - 1, c.bit_length() - 1), (1, 1), (0, c.bit_length() - 1)):
+        y = T.transform_2d(x, w, lm, ln, True, ctx)
+        yr = oracle.transform_2d("fwt", True, w, x, lm, ln)
+        assert_exact(y, yr, "2d fwd %s %s" % (wname, shape))
+        assert_exact(T.transform_2d(yr, w, lm, ln, False, ctx),
+                     oracle.transform_2d("fwt", False, w, yr, lm, ln), "2d rev")
+
+
+@pytest.mark.parametrize("wname", ["Haar1", "Daubechies4", "Symlet8"])
+def test_wpt2d(ctx, wname):
+    w = jw.by_class(wname)
+    x = rnd(64 * 128, 9).reshape(64, 128)
+    y = T.transform_2d(x, w, 6, 7, True, ctx, kind="wpt")
+    yr = oracle.transform_2d("wpt", True, w, x, 6, 7)
+    assert_exact(y, yr, "wpt2d fwd")
+    assert_exact(T.transform_2d(yr, w, 6, 7, False, ctx, kind="wpt"),
+                 oracle.transform_2d("wpt", False, w, yr, 6, 7), "wpt2d rev")
+
+
+@pytest.mark.parametrize("wname", ["Haar1", "Daubechies4", "Daubechies8"])
+@pytest.mark.parametrize("shape", [(2, 4, 8), (16, 32, 64), (8, 8, 8), (64, 16, 2048)])
+def test_3d(ctx, wname, shape):
+    w = jw.by_class(wname)
+    p, q, r = shape
+    x = rnd(p * q * r, 17).reshape(shape)
+    # levels as the reference applies them: (lvlP on Q, lvlQ on R, lvlR on P)
+    lp, lq, lr = q.bit_length() - 1, r.bit_length() - 1, p.bit_length() - 1
+    y = T.transform_3d(x, w, lp, lq, lr, True, ctx)
+    yr = oracle.transform_3d("fwt", True, w, x, lp, lq, lr)
+    assert_exact(y, yr, "3d fwd")
+    assert_exact(T.transform_3d(yr, w, lp, lq, lr, False, ctx),
+                 oracle.transform_3d("fwt", False, w, yr, lp, lq, lr), "3d rev")
+
+
+# ------------------------------------------------------------------ MODWT
+@pytest.mark.parametrize("wname", ["Haar1", "Daubechies2", "Daubechies4", "Daubechies8",
+                                   "Symlet8", "Coiflet1", "Daubechies20", "CDF53"])
+def test_modwt(ctx, wname):
+    w = jw.by_class(wname)
+    for n in (2, 3, 8, 100, 288, 500, 1000, 4097, 12345):
+        x = rnd(n, n)
+        for J in sorted({1, min(4, n.bit_length() - 1), min(8, n.bit_length() - 1)}):
+            c = T.modwt_forward(x, w, J, ctx)
+            cr = oracle.modwt_forward(w, x, J)
+            assert_exact(c, cr, "%s modwt fwd n=%d J=%d" % (wname, n, J))
+            xr = T.modwt_inverse(cr, w, ctx)
+            assert_exact(xr, oracle.modwt_inverse(w, cr), "%s modwt inv n=%d J=%d" % (wname, n, J))
+
+
+def test_modwt_deep_levels(ctx):
+    """Levels whose halo exceeds one tile run per level (J up to 13)."""
+    w = jw.by_class("Daubechies4")
+    n = 20000
+    x = rnd(n, 1)
+    for J in (10, 13):
+        c = T.modwt_forward(x, w, J, ctx)
+        cr = oracle.modwt_forward(w, x, J)
+        assert_exact(c, cr, "modwt J=%d" % J)
+        assert_exact(T.modwt_inverse(cr, w, ctx), oracle.modwt_inverse(w, cr), "imodwt J=%d" % J)
+
+
+def test_modwt_config5_full_size(ctx, ctx_fma):
+    """Config 5: Daubechies4, J=8, N=10^7 — exact vs oracle; round trip."""
+    w = jw.by_class("Daubechies4")
+    n = 10_000_000
+    x = rnd(n, 42)
+    c = T.modwt_forward(x, w, 8, ctx)
+    cr = oracle.modwt_forward(w, x, 8)
+    assert_exact(c, cr, "modwt 1e7")
+    xr = T.modwt_inverse(c, w, ctx)
+    assert_exact(xr, oracle.modwt_inverse(w, cr), "imodwt 1e7")
+    assert np.abs(xr - x).max() < 1e-10
+    assert_close(T.modwt_forward(x, w, 8, ctx_fma), cr, "modwt fma")
+
+
+def test_modwt_direct_vs_sparse_oracle():
+    """The oracle's zero-tap-skipping loop equals the as-written DIRECT loop bit for bit."""
+    w = jw.by_class("Daubechies4")
+    x = rnd(300, 3)
+    assert_exact(oracle.modwt_forward(w, x, 5, sparse=True), oracle.modwt_forward(w, x, 5, sparse=False))
+
+
+# ------------------------------------------------------------------ KATs on GPU
+def test_haar_kat_gpu(ctx):
+    """CrossValidationTest.testHaarTransformWithReference (CrossValidationTest.java:187-211)."""
+    import os
+    g = os.path.join(os.path.dirname(__file__), "golden")
+    x = np.loadtxt(os.path.join(g, "haar_simple_input.txt"))
+    a = np.loadtxt(os.path.join(g, "haar_level1_approx_manual.txt"))
+    d = np.loadtxt(os.path.join(g, "haar_level1_detail_manual.txt"))
+    y = T.fwt_forward(x, jw.by_class("Haar1"), 1, ctx)
+    assert np.abs(y[:4] - a).max() < 1e-10 and np.abs(y[4:] - d).max() < 1e-10
+
+
+def test_modwt_haar_kat_gpu(ctx):
+    """MODWTTransformTest.testKnownValuesWithHaar (MODWTTransformTest.java:39-72)."""
+    x = np.arange(1.0, 9.0)
+    c = T.modwt_forward(x, jw.by_class("Haar1"), 1, ctx)
+    assert np.abs(c[0] - np.array([-3.5] + [0.5] * 7)).max() < 1e-9
+    assert np.abs(c[1] - np.array([4.5, 1.5, 2.5, 3.5, 4.5, 5.5, 6.5, 7.5])).max() < 1e-9
+
+
+# ------------------------------------------------------------------ C ABI errors
+def test_native_validation_messages(ctx):
+    w = jw.by_class("Daubechies4")
+    with pytest.raises(jw.JWaveFailure, match="FastWaveletTransform#forward - given array length"):
+        T.fwt_forward(np.zeros(12), w, 1, ctx)
+    with pytest.raises(jw.JWaveFailure, match="given level is out of range"):
+        T.fwt_forward(np.zeros(16), w, 5, ctx)
+    with pytest.raises(jw.JWaveFailure, match="WaveletPacketTransform#reverse"):
+        T.wpt_reverse(np.zeros(16), w, -1, ctx)
+    with pytest.raises(ValueError, match="theoretical limit 3"):
+        T.modwt_forward(np.zeros(10), w, 4, ctx)
+    with pytest.raises(ValueError, match="maximum supported decomposition level is 13"):
+        T.modwt_forward(np.zeros(1 << 15), w, 14, ctx)
+
+
+def test_single_hip_runtime(ctx):
+    """torch and libjwave_hip.so share one HIP runtime in the process."""
+    import torch
+    from jwave_amd import _lib
+    assert torch.cuda.is_available()
+    maps = _lib.hip_runtimes_mapped()
+    assert len(maps) == 1, maps
+
+
+def test_device_tensors_and_stream(ctx):
+    """torch CUDA tensors go through the _dev entry points on torch's stream."""
+    import torch
+    w = jw.by_class("Daubechies4")
+    x = rnd(1 << 16, 4)
+    xt = torch.from_numpy(x).cuda()
+    y = T.fwt_forward(xt, w, 16, ctx)
+    xr = T.fwt_reverse(y, w, 16, ctx)
+    torch.cuda.synchronize()
+    yr = oracle.fwt_forward(w, x, 16)
+    assert_exact(y.cpu().numpy(), yr, "dev fwd")
+    assert_exact(xr.cpu().numpy(), oracle.fwt_reverse(w, yr, 16), "dev rev")
+
+
+def test_facade_and_classes(ctx):
+    """SteppingTest-style use of the operator mirror (SteppingTest.java:55-80)."""
+    for w in jw.WaveletBuilder.create2arr():
+        t = jw.Transform(jw.FastWaveletTransform(w, ctx))
+        x = np.ones(4)
+        s2 = np.sqrt(2.0)
+        np.testing.assert_allclose(t.forward(x, 0), [1, 1, 1, 1], atol=1e-8)
+        np.testing.assert_allclose(t.forward(x, 1), [s2, s2, 0, 0], atol=1e-8)
+        np.testing.assert_allclose(t.forward(x, 2), [2, 0, 0, 0], atol=1e-8)
+        for lev in (0, 1, 2):
+            np.testing.assert_allclose(t.reverse(t.forward(x, lev), lev), x, atol=1e-8)
+    assert jw.Transform(jw.FastWaveletTransform(jw.by_class("Haar1"), ctx)).forward(np.ones(3)) is None

@@ -1,0 +1,267 @@
+"""CPU tests: the oracle against the reference's own KATs / fixtures, against an
+independent numpy restatement, and against the committed golden vectors; the
+filter-bank data; the host mirror's validation; the C ABI exports.
+
+No GPU needed (the native library is loaded but no compute call is made).
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import numpy_restatement as npr
+import jwave_amd as jw
+from jwave_amd import _lib
+from jwave_amd.wavelets import WaveletBuilder
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+CREATE2ARR = WaveletBuilder.create2arr()
+
+
+def load_vec(name):
+    return np.loadtxt(os.path.join(GOLDEN, name))
+
+
+# ----------------------------------------------------------- taps / fixtures
+def test_haar_taps_fixture():
+    """CrossValidationTest.testHaarWaveletCoefficients (CrossValidationTest.java:159-184)."""
+    w = jw.by_class("Haar1")
+    np.testing.assert_allclose(w.getScalingDeComposition(), load_vec("filter_haar_dec_lo.txt"), atol=1e-10)
+    np.testing.assert_allclose(w.getWaveletDeComposition(), load_vec("filter_haar_dec_hi.txt"), atol=1e-10)
+    np.testing.assert_allclose(w.getScalingReConstruction(), load_vec("filter_haar_rec_lo.txt"), atol=1e-10)
+
+
+def test_db2_fixture_matches_daubechies2():
+    """filter_db4_dec_lo.txt is PyWavelets' db2 == JWave Daubechies2 (4 taps)."""
+    np.testing.assert_allclose(jw.by_class("Daubechies2").lo, load_vec("filter_db4_dec_lo.txt"), atol=1e-12)
+
+
+@pytest.mark.parametrize("w", CREATE2ARR, ids=lambda w: w.name)
+def test_filter_bank_shape(w):
+    L = w.mother_wavelength
+    assert len(w.lo) == len(w.hi) == len(w.lo_r) == len(w.hi_r) == L
+    assert w.transform_wavelength == 2
+
+
+def test_config_wavelets_orthonormal_to_tap_precision():
+    # the reference taps are orthonormal only to ~1e-12
+    for cls, bound in (("Haar1", 1e-15), ("Daubechies4", 1e-12), ("Daubechies8", 3e-12),
+                       ("Symlet8", 1e-12)):
+        w = jw.by_class(cls)
+        assert abs(sum(c * c for c in w.lo) - 1.0) < bound
+
+
+def test_builder_refusals():
+    for name in ("Battle 23", "CDF 5/3", "CDF 9/7"):
+        with pytest.raises(jw.JWaveFailure, match="odd number of coefficients"):
+            WaveletBuilder.create(name)
+    with pytest.raises(jw.JWaveFailure, match="unknown type of wavelet"):
+        WaveletBuilder.create("Nope 7")
+    assert len(CREATE2ARR) == 52
+
+
+# ----------------------------------------------------------------- KATs
+def test_haar_level1_kat():
+    """CrossValidationTest.testHaarTransformWithReference (:187-211), tol 1e-10."""
+    x = load_vec("haar_simple_input.txt")
+    y = oracle.fwt_forward(jw.by_class("Haar1"), x, 1)
+    np.testing.assert_allclose(y[:4], load_vec("haar_level1_approx_manual.txt"), atol=1e-10)
+    np.testing.assert_allclose(y[4:], load_vec("haar_level1_detail_manual.txt"), atol=1e-10)
+
+
+def test_modwt_haar_kat():
+    """MODWTTransformTest.testKnownValuesWithHaar (MODWTTransformTest.java:39-72)."""
+    c = oracle.modwt_forward(jw.by_class("Haar1"), np.arange(1.0, 9.0), 1, sparse=False)
+    np.testing.assert_allclose(c[0], [-3.5] + [0.5] * 7, atol=1e-9)
+    np.testing.assert_allclose(c[1], [4.5, 1.5, 2.5, 3.5, 4.5, 5.5, 6.5, 7.5], atol=1e-9)
+    g, h = oracle.modwt_filters(jw.by_class("Haar1"))
+    np.testing.assert_allclose(g, [0.5, 0.5], atol=1e-15)
+    np.testing.assert_allclose(h, [0.5, -0.5], atol=1e-15)
+
+
+def _stepping_expect(n, p):
+    e = np.zeros(n)
+    e[: n >> p] = 2.0 ** (p / 2.0)
+    return e
+
+
+@pytest.mark.parametrize("w", CREATE2ARR, ids=lambda w: w.name)
+def test_stepping_kat(w):
+    """SteppingTest.testStepping (SteppingTest.java:37-315): constant signals,
+    FWT and WPT, level-p energy 2^(p/2) in the first N/2^p slots, delta 1e-8."""
+    for n in (4, 64):
+        x = np.ones(n)
+        for p in range(0, n.bit_length()):
+            y = oracle.fwt_forward(w, x, p)
+            np.testing.assert_allclose(y, _stepping_expect(n, p), atol=1e-8)
+            np.testing.assert_allclose(oracle.fwt_reverse(w, y, p), x, atol=1e-8)
+            yw = oracle.wpt_forward(w, x, p)
+            np.testing.assert_allclose(yw, _stepping_expect(n, p), atol=1e-8)
+            np.testing.assert_allclose(oracle.wpt_reverse(w, yw, p), x, atol=1e-8)
+
+
+@pytest.mark.parametrize("w", CREATE2ARR[:20] + CREATE2ARR[25:32], ids=lambda w: w.name)
+def test_general_roundtrip(w):
+    """GeneralTest.testExample (GeneralTest.java:36-80): fixed 8-vector round trip."""
+    x = np.array([1., 2., 3., 4., 5., 6., 7., 8.])
+    y = oracle.fwt_forward(w, x, 3)
+    np.testing.assert_allclose(oracle.fwt_reverse(w, y, 3), x, atol=1e-6)
+
+
+def test_property_linearity_energy():
+    """PropertyBasedTest (PropertyBasedTest.java:138-382) on the oracle, Random(42)."""
+    for cls in ("Haar1", "Daubechies4", "Symlet4"):
+        w = jw.by_class(cls)
+        x = oracle.java_random_doubles(42, 256)
+        z = oracle.java_random_doubles(43, 256)
+        a = 3.25
+        fx, fz = oracle.fwt_forward(w, x, 8), oracle.fwt_forward(w, z, 8)
+        np.testing.assert_allclose(oracle.fwt_forward(w, a * x + z, 8), a * fx + fz, atol=1e-8)
+        assert abs(np.dot(fx, fx) - np.dot(x, x)) < 1e-8 * np.dot(x, x)
+
+
+def test_java_random_matches_reference_algorithm():
+    """java.util.Random(42).nextDouble() first values (the LCG of the JDK spec)."""
+    v = oracle.java_random_doubles(42, 3)
+    assert v[0] == 0.7275636800328681 and v[1] == 0.6832234717598454 and v[2] == 0.30871945533265976
+
+
+# ------------------------------------------------- oracle vs numpy (bitwise)
+@pytest.mark.parametrize("cls", ["Haar1", "Daubechies4", "Daubechies8", "Symlet8", "Coiflet1",
+                                 "Haar1Orthogonal", "CDF53", "Battle23", "BiOrthogonal35",
+                                 "DiscreteMeyer"])
+def test_oracle_equals_numpy_restatement(cls):
+    w = jw.by_class(cls)
+    for n in (2, 8, 64, 512):
+        x = oracle.java_random_doubles(n, n)
+        for lev in range(0, n.bit_length()):
+            y = oracle.fwt_forward(w, x, lev)
+            assert np.array_equal(y, npr.fwt_forward(w, x, lev))
+            assert np.array_equal(oracle.fwt_reverse(w, y, lev), npr.fwt_reverse(w, y, lev))
+            yw = oracle.wpt_forward(w, x, lev)
+            assert np.array_equal(yw, npr.wpt_forward(w, x, lev))
+            assert np.array_equal(oracle.wpt_reverse(w, yw, lev), npr.wpt_reverse(w, yw, lev))
+
+
+@pytest.mark.parametrize("cls", ["Haar1", "Daubechies4", "Symlet8", "CDF53"])
+def test_oracle_modwt_equals_numpy(cls):
+    w = jw.by_class(cls)
+    for n, J in ((8, 3), (100, 5), (1000, 8), (37, 2)):
+        x = oracle.java_random_doubles(7, n)
+        c = oracle.modwt_forward(w, x, J, sparse=False)
+        assert np.array_equal(c, oracle.modwt_forward(w, x, J, sparse=True))
+        assert np.array_equal(c, npr.modwt_forward(w, x, J))
+        assert np.array_equal(oracle.modwt_inverse(w, c), npr.modwt_inverse(w, c))
+    assert np.array_equal(np.stack(oracle.modwt_filters(w)), np.stack(npr.modwt_filters(w)))
+
+
+def test_oracle_2d_3d_equal_loops():
+    """2-D/3-D oracle == explicit per-line loops of the 1-D oracle (BasicTransform.java:361-659)."""
+    w = jw.by_class("Daubechies4")
+    x = oracle.java_random_doubles(5, 16 * 32).reshape(16, 32)
+    y = np.array([oracle.fwt_forward(w, r, 3) for r in x])
+    y = np.array([oracle.fwt_forward(w, c, 2) for c in y.T]).T
+    assert np.array_equal(oracle.transform_2d("fwt", True, w, x, 2, 3), y)
+    s = oracle.java_random_doubles(6, 4 * 8 * 16).reshape(4, 8, 16)
+    ref = np.stack([oracle.transform_2d("fwt", True, w, s[i], 3, 4) for i in range(4)])
+    ref = np.apply_along_axis(lambda v: oracle.fwt_forward(w, v, 2), 0, ref)
+    assert np.array_equal(oracle.transform_3d("fwt", True, w, s, 3, 4, 2), ref)
+
+
+# --------------------------------------------------------------- golden vectors
+def _check(rec, a):
+    a = np.ascontiguousarray(np.asarray(a, dtype="<f8"))
+    assert list(a.shape) == rec["shape"]
+    assert hashlib.sha256(a.tobytes()).hexdigest() == rec["sha256"]
+    if "hex" in rec:
+        assert [float(v).hex() for v in a.ravel()] == rec["hex"]
+
+
+def test_golden_vectors():
+    data = json.load(open(os.path.join(GOLDEN, "golden.json")))
+    for case in data["cases"]:
+        w = jw.by_class(case["wavelet"])
+        op = case["op"]
+        if op == "fwt":
+            x = oracle.java_random_doubles(case["seed"], case["n"])
+            y = oracle.fwt_forward(w, x, case["level"])
+            _check(case["forward"], y)
+            _check(case["roundtrip"], oracle.fwt_reverse(w, y, case["level"]))
+        elif op == "fwt2d":
+            r, c = case["shape"]
+            x = oracle.java_random_doubles(case["seed"], r * c).reshape(r, c)
+            y = oracle.transform_2d("fwt", True, w, x, *case["levels"])
+            _check(case["forward"], y)
+            _check(case["roundtrip"], oracle.transform_2d("fwt", False, w, y, *case["levels"]))
+        elif op == "wpt_batch":
+            x = np.stack([oracle.java_random_doubles(case["seed"] + b, case["n"])
+                          for b in range(case["batch"])])
+            y = oracle.batch("wpt", True, w, x, case["level"])
+            _check(case["forward"], y)
+            _check(case["roundtrip"], oracle.batch("wpt", False, w, y, case["level"]))
+        elif op == "modwt":
+            x = oracle.java_random_doubles(case["seed"], case["n"])
+            c = oracle.modwt_forward(w, x, case["level"])
+            _check(case["forward"], c)
+            _check(case["roundtrip"], oracle.modwt_inverse(w, c))
+
+
+# ----------------------------------------------------------- host mirror (no GPU)
+def test_mirror_validation_messages():
+    w = jw.by_class("Daubechies4")
+    fwt = jw.FastWaveletTransform(w)
+    with pytest.raises(jw.JWaveFailure, match=r"^FastWaveletTransform#forward - given array length"):
+        fwt.forward(np.zeros(12), 2)
+    with pytest.raises(jw.JWaveFailure, match=r"^FastWaveletTransform#reverse - given level is out"):
+        fwt.reverse(np.zeros(16), 5)
+    with pytest.raises(jw.JWaveFailure, match=r"^WaveletTransform#forward - given array length"):
+        fwt.forward(np.zeros(12))
+    wpt = jw.WaveletPacketTransform(w)
+    with pytest.raises(jw.JWaveFailure, match=r"^WaveletPacketTransform#forward - given level"):
+        wpt.forward(np.zeros(16), 7)
+    with pytest.raises(jw.JWaveFailure, match="invalid level"):
+        jw.PooledWaveletPacketTransform(w).forward(np.zeros(16), 0)
+    m = jw.MODWTTransform(w)
+    with pytest.raises(ValueError, match="at least 1"):
+        m.forwardMODWT(np.zeros(8), 0)
+    with pytest.raises(ValueError, match="maximum supported decomposition level is 13"):
+        m.forwardMODWT(np.zeros(8), 14)
+    with pytest.raises(ValueError, match="exceeds theoretical limit 3 for signal length 10"):
+        m.forwardMODWT(np.zeros(10), 4)
+    assert m.forwardMODWT(np.zeros(0), 3).shape == (4, 0)
+    assert m.inverseMODWT(np.zeros((1, 5))).shape == (0,)
+    # the facade prints and returns None (Transform.java:81-90)
+    assert jw.Transform(fwt).forward(np.zeros(12), 1) is None
+
+
+# ------------------------------------------------------------------- C ABI
+def test_abi_exports_every_header_symbol():
+    lib = _lib.lib()
+    syms = _lib.header_symbols()
+    assert len(syms) >= 40
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    assert lib.jwv_version() >= 100
+
+
+def test_abi_no_device_reports_error():
+    """Without a GPU the library loads and refuses a context loudly (no CPU fallback)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import ctypes
+    lib = _lib.lib()
+    h = ctypes.c_void_p()
+    assert lib.jwv_ctx_create(0, ctypes.byref(h)) == _lib.JWV_ERR_DEVICE
+    assert b"device" in lib.jwv_last_error(None)
+    with pytest.raises(jw.JWaveError):
+        jw.Context(0)
+
+
+def test_abi_modwt_filters_host_only():
+    g, h = jw.modwt_filters(jw.by_class("Daubechies4"))
+    go, ho = oracle.modwt_filters(jw.by_class("Daubechies4"))
+    assert np.array_equal(g, go) and np.array_equal(h, ho)
