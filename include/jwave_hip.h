@@ -74,8 +74,11 @@ int jwv_ctx_destroy(jwv_ctx* ctx);
 /* Last error message of this context ("" if none).  ctx may be NULL: then the
  * calling thread's last context-less error (e.g. from jwv_ctx_create). */
 const char* jwv_last_error(const jwv_ctx* ctx);
-/* Use a caller-owned hipStream_t (NULL = the context's own stream). */
+/* Launch on a caller-owned hipStream_t (NULL = the legacy default stream);
+ * jwv_ctx_reset_stream returns to the context's own non-blocking stream
+ * (the default after jwv_ctx_create). */
 int jwv_ctx_set_stream(jwv_ctx* ctx, void* hip_stream);
+int jwv_ctx_reset_stream(jwv_ctx* ctx);
 void* jwv_ctx_get_stream(const jwv_ctx* ctx);
 int jwv_ctx_set_math(jwv_ctx* ctx, int mode);
 int jwv_ctx_synchronize(jwv_ctx* ctx);

@@ -53,6 +53,7 @@ _SIGS = {
     "jwv_ctx_destroy": [_CTX],
     "jwv_last_error": [_CTX],
     "jwv_ctx_set_stream": [_CTX, ctypes.c_void_p],
+    "jwv_ctx_reset_stream": [_CTX],
     "jwv_ctx_get_stream": [_CTX],
     "jwv_ctx_set_math": [_CTX, _int],
     "jwv_ctx_synchronize": [_CTX],

@@ -198,6 +198,14 @@ void copy_axis(jwv_ctx* c, const Axis& a) {
 
 int col_slab(int inner) { return inner == 1 ? 1 : 8; }
 
+// LDS-DMA (16 B per lane) needs 16-B aligned rows / row pairs.
+bool dma_view(const double* base, const AxisView& v, int C, int inner) {
+  if (((uintptr_t)base & 15) != 0) return false;
+  if ((v.s_outer & 1) || (v.pk > 1 && (v.s_pk & 1))) return false;
+  if (C == 1) return v.s_len == 1;
+  return (v.s_len & 1) == 0 && inner % C == 0;
+}
+
 // Number of levels FastWaveletTransform / WaveletPacketTransform.forward runs
 // (FastWaveletTransform.java:90: while h >= transformWavelength && l < level).
 int fwd_levels(int len, int tw, int level) {
@@ -238,7 +246,8 @@ void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
     const bool last = K == rem;
     double* ad = last ? a.dst : c->ws[pp].p;
     const AxisView av = last ? a.dv : cview(h >> K, a.inner);
-    jwv::TileArgs t{cur, cv, nullptr, {}, a.dst, a.dv, ad, av, h, K, a.outer, a.inner};
+    jwv::TileArgs t{cur, cv, nullptr, {}, a.dst, a.dv, ad, av, h, K, a.outer, a.inner,
+                    dma_view(cur, cv, C, a.inner)};
     { ProfScope ps_(c, K_FWT_FWD_TILE, 16.0 * a.outer * h * a.inner);
     hipchk(jwv::launch_fwt_fwd_tile(b, use_fma(c), C, t, c->stream), "fwt_fwd_tile"); }
     cur = ad;
@@ -248,7 +257,7 @@ void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
     pp ^= 1;
   }
   if (rem > 0) {
-    jwv::ResArgs r{cur, cv, a.dst, a.dv, h, 0, rem, a.outer, a.inner};
+    jwv::ResArgs r{cur, cv, a.dst, a.dv, h, 0, rem, a.outer, a.inner, dma_view(cur, cv, C, a.inner)};
     { ProfScope ps_(c, K_FWT_FWD_RES, 16.0 * a.outer * h * a.inner);
     hipchk(jwv::launch_fwt_fwd_res(b, use_fma(c), C, r, c->stream), "fwt_fwd_res"); }
   }
@@ -286,7 +295,8 @@ void fwt_rev_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
     const bool last = hres == a.len;
     double* out = last ? a.dst : c->ws[pp].p;
     const AxisView ov = last ? a.dv : cview(hres, a.inner);
-    jwv::ResArgs r{a.src, a.sv, out, ov, h, 0, nres, a.outer, a.inner};
+    jwv::ResArgs r{a.src, a.sv, out, ov, h, 0, nres, a.outer, a.inner,
+                   dma_view(a.src, a.sv, C, a.inner)};
     { ProfScope ps_(c, K_FWT_REV_RES, 16.0 * a.outer * hres * a.inner);
     hipchk(jwv::launch_fwt_rev_res(b, use_fma(c), C, r, c->stream), "fwt_rev_res"); }
     if (last) return;
@@ -305,7 +315,8 @@ void fwt_rev_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
     const bool last = hK == a.len;
     double* out = last ? a.dst : c->ws[pp].p;
     const AxisView ov = last ? a.dv : cview(hK, a.inner);
-    jwv::TileArgs t{acur, acv, a.src, a.sv, out, ov, nullptr, {}, h1, K, a.outer, a.inner};
+    jwv::TileArgs t{acur, acv, a.src, a.sv, out, ov, nullptr, {}, h1, K, a.outer, a.inner,
+                    dma_view(acur, acv, C, a.inner) && dma_view(a.src, a.sv, C, a.inner)};
     { ProfScope ps_(c, K_FWT_REV_TILE, 16.0 * a.outer * hK * a.inner);
     hipchk(jwv::launch_fwt_rev_tile(b, use_fma(c), C, t, c->stream), "fwt_rev_tile"); }
     acur = out;
@@ -339,13 +350,15 @@ void run_wpt_passes(jwv_ctx* c, const Bank& b, const Axis& a, bool fwd,
     const AxisView sv = with_packets(cv, p.pk, p.h), dv = with_packets(ov, p.pk, p.h);
     const int64_t nouter = a.outer * p.pk;
     if (p.tiled) {
-      jwv::TileArgs t{cur, sv, nullptr, {}, out, dv, nullptr, {}, p.h, p.nlev, nouter, a.inner};
+      jwv::TileArgs t{cur, sv, nullptr, {}, out, dv, nullptr, {}, p.h, p.nlev, nouter, a.inner,
+                      dma_view(cur, sv, C, a.inner)};
       ProfScope ps_(c, fwd ? K_WPT_FWD_TILE : K_WPT_REV_TILE, 16.0 * a.outer * a.len * a.inner);
       hipchk(fwd ? jwv::launch_wpt_fwd_tile(b, use_fma(c), C, t, c->stream)
                  : jwv::launch_wpt_rev_tile(b, use_fma(c), C, t, c->stream),
              "wpt_tile");
     } else {
-      jwv::ResArgs r{cur, sv, out, dv, p.h, p.h0, p.nlev, nouter, a.inner};
+      jwv::ResArgs r{cur, sv, out, dv, p.h, p.h0, p.nlev, nouter, a.inner,
+                     dma_view(cur, sv, C, a.inner)};
       ProfScope ps_(c, fwd ? K_WPT_FWD_RES : K_WPT_REV_RES, 16.0 * a.outer * a.len * a.inner);
       hipchk(fwd ? jwv::launch_wpt_fwd_res(b, use_fma(c), C, r, c->stream)
                  : jwv::launch_wpt_rev_res(b, use_fma(c), C, r, c->stream),
@@ -705,7 +718,14 @@ const char* jwv_last_error(const jwv_ctx* c) { return c ? c->err.c_str() : g_tls
 int jwv_ctx_set_stream(jwv_ctx* c, void* s) {
   if (!c) return set_err(nullptr, JWV_ERR_BAD_CALL, "jwv_ctx is NULL");
   std::lock_guard<std::mutex> lk(c->mu);
-  c->stream = s ? (hipStream_t)s : c->own;
+  c->stream = (hipStream_t)s;  // NULL = the legacy default stream
+  return JWV_OK;
+}
+
+int jwv_ctx_reset_stream(jwv_ctx* c) {
+  if (!c) return set_err(nullptr, JWV_ERR_BAD_CALL, "jwv_ctx is NULL");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->stream = c->own;
   return JWV_OK;
 }
 

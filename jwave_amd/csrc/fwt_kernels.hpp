@@ -170,10 +170,11 @@ __device__ double rev_small(const typename FB<L>::Rev& tp, const double* a, cons
 template <int L, int C, int NT, int CAP, bool FMA>
 __global__ __launch_bounds__(NT) void fwt_fwd_res(const double* __restrict__ src, AxisView sv,
                                                   double* __restrict__ dst, AxisView dv, int h0,
-                                                  int nlev, int inner,
+                                                  int nlev, int inner, int dma,
                                                   typename FB<L>::Fwd tp) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   constexpr int MAXP = (CAP / 2 * C + NT - 1) / NT;
+  constexpr int MAXU = (CAP * C + NT - 1) / NT;
   const int ncb = (inner + C - 1) / C;
   const int64_t o = blockIdx.x / ncb;
   const int c0 = (blockIdx.x % ncb) * C;
@@ -181,11 +182,9 @@ __global__ __launch_bounds__(NT) void fwt_fwd_res(const double* __restrict__ src
   double* y = dst + view_base(dv, o) + c0;
   const int tid = threadIdx.x;
 
-  for (int q = tid; q < h0 * C; q += NT) {
-    const int i = q / C, c = q % C;
-    lds[q] = (c0 + c < inner) ? s[i * sv.s_len + c] : 0.0;
-  }
-  __syncthreads();
+  load_window<C, NT, MAXU>(lds, s, h0, dma != 0, c0, inner,
+                           [&](int e) { return (int64_t)e * sv.s_len; });
+  dma_fence_barrier();
 
   int h = h0;
   for (int lev = 0; lev < nlev; ++lev) {
@@ -229,12 +228,13 @@ template <int L, int C, int NT, int T, int KMAX, bool FMA>
 __global__ __launch_bounds__(NT) void fwt_fwd_tile(const double* __restrict__ src, AxisView sv,
                                                    double* __restrict__ dst, AxisView dv,
                                                    double* __restrict__ adst, AxisView av_,
-                                                   int h, int K, int inner,
+                                                   int h, int K, int inner, int dma,
                                                    typename FB<L>::Fwd tp) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   constexpr int LM = LMax<L>::v;
   constexpr int M0MAX = T + (LM - 2) * ((1 << KMAX) - 1);
   constexpr int MAXP = ((M0MAX - (LM - 2)) / 2 * C + NT - 1) / NT;
+  constexpr int MAXU = (M0MAX * C + NT - 1) / NT;
   const int nL = FB<L>::n(tp);
   const int ntile = h / T;
   const int ncb = (inner + C - 1) / C;
@@ -255,11 +255,9 @@ __global__ __launch_bounds__(NT) void fwt_fwd_tile(const double* __restrict__ sr
   const int m0 = T + (nL - 2) * ((1 << K) - 1);
   const int msk = h - 1;
   const int base = t * T;
-  for (int q = tid; q < m0 * C; q += NT) {
-    const int e = q / C, c = q % C;
-    lds[q] = (c0 + c < inner) ? s[(int64_t)((base + e) & msk) * sv.s_len + c] : 0.0;
-  }
-  __syncthreads();
+  load_window<C, NT, MAXU>(lds, s, m0, dma != 0, c0, inner,
+                           [&](int e) { return (int64_t)((base + e) & msk) * sv.s_len; });
+  dma_fence_barrier();
 
   int m = m0, hl = h;
   for (int l = 1; l <= K; ++l) {
@@ -304,10 +302,11 @@ __global__ __launch_bounds__(NT) void fwt_fwd_tile(const double* __restrict__ sr
 template <int L, int C, int NT, int CAP, bool FMA>
 __global__ __launch_bounds__(NT) void fwt_rev_res(const double* __restrict__ src, AxisView sv,
                                                   double* __restrict__ dst, AxisView dv, int h0,
-                                                  int nlev, int inner,
+                                                  int nlev, int inner, int dma,
                                                   typename FB<L>::Rev tp) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   constexpr int MAXP = (CAP / 2 * C + NT - 1) / NT;
+  constexpr int MAXU = (CAP * C + NT - 1) / NT;
   const int nL = FB<L>::nr(tp);
   const int ncb = (inner + C - 1) / C;
   const int64_t o = blockIdx.x / ncb;
@@ -317,11 +316,9 @@ __global__ __launch_bounds__(NT) void fwt_rev_res(const double* __restrict__ src
   const int tid = threadIdx.x;
   const int htop = nlev > 0 ? (h0 << (nlev - 1)) : h0;
 
-  for (int q = tid; q < htop * C; q += NT) {
-    const int i = q / C, c = q % C;
-    lds[q] = (c0 + c < inner) ? s[(int64_t)i * sv.s_len + c] : 0.0;
-  }
-  __syncthreads();
+  load_window<C, NT, MAXU>(lds, s, htop, dma != 0, c0, inner,
+                           [&](int e) { return (int64_t)e * sv.s_len; });
+  dma_fence_barrier();
 
   int h = h0;
   for (int lev = 0; lev < nlev; ++lev) {
@@ -380,12 +377,14 @@ template <int L, int C, int NT, int T, int KMAX, bool FMA>
 __global__ __launch_bounds__(NT) void fwt_rev_tile(const double* __restrict__ asrc, AxisView as,
                                                    const double* __restrict__ coef, AxisView cv,
                                                    double* __restrict__ dst, AxisView dv, int h1,
-                                                   int K, int inner, typename FB<L>::Rev tp) {
+                                                   int K, int inner, int dma,
+                                                   typename FB<L>::Rev tp) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   constexpr int LM = LMax<L>::v;
   constexpr int QM = (LM + 1) / 2;
   constexpr int WMAX = T / 2 + 2 * QM + 4;  // max window (pairs*2) at level >= 1
   constexpr int MAXP = ((T / 2 + QM + 2) * C + NT - 1) / NT;
+  constexpr int MAXU = (WMAX * C + NT - 1) / NT;
   const int nL = FB<L>::nr(tp);
   const int Q = (nL + 1) >> 1;
   const int hK = h1 << (K - 1);
@@ -418,23 +417,18 @@ __global__ __launch_bounds__(NT) void fwt_rev_tile(const double* __restrict__ as
     const int BK = win_b(K);
     const int W = win_e(K) - BK;
     const int am = (hK >> K) - 1;
-    for (int q = tid; q < W * C; q += NT) {
-      const int e = q / C, c = q % C;
-      abuf[q] = (c0 + c < inner) ? sa[(int64_t)((BK + e) & am) * as.s_len + c] : 0.0;
-    }
+    load_window<C, NT, MAXU>(abuf, sa, W, dma != 0, c0, inner,
+                             [&](int e) { return (int64_t)((BK + e) & am) * as.s_len; });
   }
   for (int l = K - 1; l >= 0; --l) {
     // level with output size hl = hK >> l; inputs a,d of length half = hl/2
     const int half = hK >> (l + 1), hm = half - 1;
     const int Bl = win_b(l), Bl1 = win_b(l + 1);
     const int Wd = win_e(l + 1) - Bl1;
-    for (int q = tid; q < Wd * C; q += NT) {
-      const int e = q / C, c = q % C;
-      dbuf[q] = (c0 + c < inner)
-                    ? sc[((int64_t)half + ((Bl1 + e) & hm)) * cv.s_len + c]
-                    : 0.0;
-    }
-    __syncthreads();
+    load_window<C, NT, MAXU>(dbuf, sc, Wd, dma != 0, c0, inner, [&](int e) {
+      return ((int64_t)half + ((Bl1 + e) & hm)) * cv.s_len;
+    });
+    dma_fence_barrier();
     const int pbase = Bl >> 1;                     // first pair (global, may be <0)
     const int np = ((win_e(l) - Bl) >> 1) * C;     // pairs in window
     const int off = pbase - Bl1;                   // local index of a[pbase]

@@ -58,6 +58,59 @@ struct AnyTaps {
   int32_t pad_;
 };
 
+// Wait for this wave's LDS-DMA loads, then a workgroup barrier: after it
+// every wave sees every other wave's DMA'd rows in LDS.
+__device__ __forceinline__ void dma_fence_barrier() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
+// Load a window of W rows (C doubles each; row e from global src + rowoff(e),
+// columns contiguous) into lds[e*C + c].
+//  dma = 1: LDS-DMA, 16 B per lane (global_load_lds_dwordx4): every request in
+//           flight at once, no VGPRs.  Requires src + rowoff(e) 16-B aligned for
+//           even e (C=1) / every e (C>=2), C even or 1, and that for C=1 the
+//           pair (e, e+1) is contiguous in global memory; reads one row past W
+//           when W is odd (LDS must have room; global row must exist).
+//  dma = 0: plain loads, all issued before the first LDS write (MAXU bound).
+// Columns c0+c >= inner are zero-filled (register path) or skipped (dma path
+// is only used when the slab is complete).  Caller issues dma_fence_barrier().
+template <int C, int NT, int MAXU, typename RowOff>
+__device__ __forceinline__ void load_window(double* lds, const double* __restrict__ src, int W,
+                                            bool dma, int c0, int inner, RowOff rowoff) {
+  const int tid = threadIdx.x;
+  if (dma) {
+    const int lane = tid & 63, wave = tid >> 6;
+    constexpr int UPR = C == 1 ? 1 : C / 2;  // 16-B units per row (C >= 2)
+    const int nunits = C == 1 ? (W + 1) >> 1 : W * UPR;
+    for (int u0 = wave * 64; u0 < nunits; u0 += NT) {
+      const int u = u0 + lane;
+      if (u < nunits) {
+        const double* g = C == 1 ? src + rowoff(2 * u) : src + rowoff(u / UPR) + (u % UPR) * 2;
+        __builtin_amdgcn_global_load_lds(
+            (const void*)g, (__attribute__((address_space(3))) void*)(lds + 2 * u0), 16, 0, 0);
+      }
+    }
+    return;
+  }
+  const int total = W * C;
+  double v[MAXU];
+#pragma unroll
+  for (int r = 0; r < MAXU; ++r) {
+    const int q = tid + r * NT;
+    v[r] = 0.0;
+    if (q < total) {
+      const int e = q / C, c = q % C;
+      if (c0 + c < inner) v[r] = src[rowoff(e) + c];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < MAXU; ++r) {
+    const int q = tid + r * NT;
+    if (q < total) lds[q] = v[r];
+  }
+}
+
 template <bool FMA>
 __device__ __forceinline__ double mac(double acc, double a, double b) {
   if constexpr (FMA) {

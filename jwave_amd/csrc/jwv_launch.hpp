@@ -36,6 +36,7 @@ struct ResArgs {  // resident FWT/WPT kernels
   int nlev;
   int64_t nouter;
   int inner;
+  int dma;     // 1: windows may be loaded with LDS-DMA (alignment checked by host)
 };
 struct TileArgs {  // tiled FWT/WPT kernels
   const double* src; AxisView sv;   // level input (fwd) / approximation (FWT rev) / bands (WPT rev)
@@ -46,6 +47,7 @@ struct TileArgs {  // tiled FWT/WPT kernels
   int K;
   int64_t nouter;
   int inner;
+  int dma;
 };
 struct ModwtArgs {
   const double* src;  // fwd: V_{j0-1}; inv: V_{j1}

@@ -66,37 +66,53 @@ template <int C> constexpr int wpt_K() { return C == 1 ? Geo::kWptK1 : Geo::kWpt
 inline unsigned ncb(int inner, int C) { return (unsigned)((inner + C - 1) / C); }
 
 // ------------------------------------------------------------- FWT
-template <int L, int C>
-hipError_t fwt_fwd_res_go(const Bank& b, const ResArgs& a, hipStream_t s) {
-  auto k = fwt_fwd_res<L, C, NT, cap<C>(), kFMA>;
-  const size_t lds = (size_t)a.n * C * sizeof(double);
+// A single-signal tail (few blocks) is latency-bound: give it 1024 threads.
+constexpr int kBigNT = 1024;
+inline bool few_blocks(const ResArgs& a, int C) { return C == 1 && a.nouter * ncb(a.inner, C) < 64; }
+
+template <int L, int C, int NTX>
+hipError_t fwt_fwd_res_nt(const Bank& b, const ResArgs& a, hipStream_t s) {
+  auto k = fwt_fwd_res<L, C, NTX, cap<C>(), kFMA>;
+  const size_t lds = (size_t)(a.n + 2) * C * sizeof(double);
   if (hipError_t e = prep(k, lds)) return e;
   const dim3 grid((unsigned)(a.nouter * ncb(a.inner, C)));
-  hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.sv, a.dst, a.dv, a.n, a.nlev, a.inner,
-                     fwd_taps<L>(b));
+  hipLaunchKernelGGL(k, grid, dim3(NTX), lds, s, a.src, a.sv, a.dst, a.dv, a.n, a.nlev, a.inner,
+                     a.dma, fwd_taps<L>(b));
+  return hipGetLastError();
+}
+template <int L, int C>
+hipError_t fwt_fwd_res_go(const Bank& b, const ResArgs& a, hipStream_t s) {
+  if constexpr (C == 1)
+    if (few_blocks(a, C)) return fwt_fwd_res_nt<L, C, kBigNT>(b, a, s);
+  return fwt_fwd_res_nt<L, C, NT>(b, a, s);
+}
+template <int L, int C, int NTX>
+hipError_t fwt_rev_res_nt(const Bank& b, const ResArgs& a, hipStream_t s) {
+  auto k = fwt_rev_res<L, C, NTX, cap<C>(), kFMA>;
+  const int htop = a.nlev > 0 ? (a.n << (a.nlev - 1)) : a.n;
+  const size_t lds = (size_t)(htop + 2) * C * sizeof(double);
+  if (hipError_t e = prep(k, lds)) return e;
+  const dim3 grid((unsigned)(a.nouter * ncb(a.inner, C)));
+  hipLaunchKernelGGL(k, grid, dim3(NTX), lds, s, a.src, a.sv, a.dst, a.dv, a.n, a.nlev, a.inner,
+                     a.dma, rev_taps<L>(b));
   return hipGetLastError();
 }
 template <int L, int C>
 hipError_t fwt_rev_res_go(const Bank& b, const ResArgs& a, hipStream_t s) {
-  auto k = fwt_rev_res<L, C, NT, cap<C>(), kFMA>;
-  const int htop = a.nlev > 0 ? (a.n << (a.nlev - 1)) : a.n;
-  const size_t lds = (size_t)htop * C * sizeof(double);
-  if (hipError_t e = prep(k, lds)) return e;
-  const dim3 grid((unsigned)(a.nouter * ncb(a.inner, C)));
-  hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.sv, a.dst, a.dv, a.n, a.nlev, a.inner,
-                     rev_taps<L>(b));
-  return hipGetLastError();
+  if constexpr (C == 1)
+    if (few_blocks(a, C)) return fwt_rev_res_nt<L, C, kBigNT>(b, a, s);
+  return fwt_rev_res_nt<L, C, NT>(b, a, s);
 }
 template <int L, int C>
 hipError_t fwt_fwd_tile_go(const Bank& b, const TileArgs& a, hipStream_t s) {
   constexpr int T = fwt_T<C>(), KM = fwt_K<C>();
   auto k = fwt_fwd_tile<L, C, NT, T, KM, kFMA>;
   const int m0 = T + (b.L - 2) * ((1 << a.K) - 1);
-  const size_t lds = (size_t)m0 * C * sizeof(double);
+  const size_t lds = (size_t)(m0 + 2) * C * sizeof(double);
   if (hipError_t e = prep(k, lds)) return e;
   const dim3 grid((unsigned)(a.nouter * ncb(a.inner, C) * (a.h / T)));
   hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.sv, a.dst, a.dv, a.adst, a.av, a.h, a.K,
-                     a.inner, fwd_taps<L>(b));
+                     a.inner, a.dma, fwd_taps<L>(b));
   return hipGetLastError();
 }
 template <int L, int C>
@@ -109,7 +125,7 @@ hipError_t fwt_rev_tile_go(const Bank& b, const TileArgs& a, hipStream_t s) {
   const int hK = a.h << (a.K - 1);
   const dim3 grid((unsigned)(a.nouter * ncb(a.inner, C) * (hK / T)));
   hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.sv, a.coef, a.cv, a.dst, a.dv, a.h, a.K,
-                     a.inner, rev_taps<L>(b));
+                     a.inner, a.dma, rev_taps<L>(b));
   return hipGetLastError();
 }
 
@@ -117,21 +133,21 @@ hipError_t fwt_rev_tile_go(const Bank& b, const TileArgs& a, hipStream_t s) {
 template <int L, int C>
 hipError_t wpt_fwd_res_go(const Bank& b, const ResArgs& a, hipStream_t s) {
   auto k = wpt_fwd_res<L, C, NT, cap<C>(), kFMA>;
-  const size_t lds = (size_t)a.n * C * sizeof(double);
+  const size_t lds = (size_t)(a.n + 2) * C * sizeof(double);
   if (hipError_t e = prep(k, lds)) return e;
   const dim3 grid((unsigned)(a.nouter * ncb(a.inner, C)));
   hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.sv, a.dst, a.dv, a.n, a.nlev, a.inner,
-                     fwd_taps<L>(b));
+                     a.dma, fwd_taps<L>(b));
   return hipGetLastError();
 }
 template <int L, int C>
 hipError_t wpt_rev_res_go(const Bank& b, const ResArgs& a, hipStream_t s) {
   auto k = wpt_rev_res<L, C, NT, cap<C>(), kFMA>;
-  const size_t lds = (size_t)a.n * C * sizeof(double);
+  const size_t lds = (size_t)(a.n + 2) * C * sizeof(double);
   if (hipError_t e = prep(k, lds)) return e;
   const dim3 grid((unsigned)(a.nouter * ncb(a.inner, C)));
   hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.sv, a.dst, a.dv, a.n, a.h0, a.nlev,
-                     a.inner, rev_taps<L>(b));
+                     a.inner, a.dma, rev_taps<L>(b));
   return hipGetLastError();
 }
 template <int L, int C>
@@ -139,11 +155,11 @@ hipError_t wpt_fwd_tile_go(const Bank& b, const TileArgs& a, hipStream_t s) {
   constexpr int T = wpt_T<C>(), KM = wpt_K<C>();
   auto k = wpt_fwd_tile<L, C, NT, T, KM, kFMA>;
   const int m0 = T + (b.L - 2) * ((1 << a.K) - 1);
-  const size_t lds = (size_t)m0 * C * sizeof(double);
+  const size_t lds = (size_t)(m0 + 2) * C * sizeof(double);
   if (hipError_t e = prep(k, lds)) return e;
   const dim3 grid((unsigned)(a.nouter * ncb(a.inner, C) * (a.h / T)));
   hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.sv, a.dst, a.dv, a.h, a.K, a.inner,
-                     fwd_taps<L>(b));
+                     a.dma, fwd_taps<L>(b));
   return hipGetLastError();
 }
 template <int L, int C>
@@ -155,7 +171,7 @@ hipError_t wpt_rev_tile_go(const Bank& b, const TileArgs& a, hipStream_t s) {
   if (hipError_t e = prep(k, lds)) return e;
   const dim3 grid((unsigned)(a.nouter * ncb(a.inner, C) * (a.h / T)));
   hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.sv, a.dst, a.dv, a.h, a.K, a.inner,
-                     rev_taps<L>(b));
+                     a.dma, rev_taps<L>(b));
   return hipGetLastError();
 }
 

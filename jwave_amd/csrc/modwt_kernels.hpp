@@ -62,7 +62,8 @@ __global__ __launch_bounds__(NT) void modwt_fwd_tile(const double* __restrict__ 
   const int64_t t0 = (int64_t)blockIdx.x * T;
   const int tid = threadIdx.x;
   const int W = T + S;
-  for (int e = tid; e < W; e += NT) lds[e] = src[wrap_mod(t0 - S + e, N)];
+  load_window<1, NT, MAXP>(lds, src, W, false, 0, 1,
+                           [&](int e) { return wrap_mod(t0 - S + e, N); });
   __syncthreads();
   int Sj = S;  // halo still carried by the level input
   for (int j = j0; j <= j1; ++j) {
@@ -139,13 +140,15 @@ __global__ __launch_bounds__(NT) void modwt_inv_tile(const double* __restrict__ 
   double* wb = lds + (T + R);
   const int64_t t0 = (int64_t)blockIdx.x * T;
   const int tid = threadIdx.x;
-  for (int e = tid; e < T + R; e += NT) vb[e] = vsrc[wrap_mod(t0 + e, N)];
+  load_window<1, NT, MAXP>(vb, vsrc, T + R, false, 0, 1,
+                           [&](int e) { return wrap_mod(t0 + e, N); });
   int Rj = R;
   for (int j = j1; j >= j0; --j) {
     const int st = 1 << (j - 1);
     const int Rn = Rj - (nL - 1) * st;
     const double* wrow = coef + (int64_t)(j - 1) * ldw;
-    for (int e = tid; e < T + Rj; e += NT) wb[e] = wrow[wrap_mod(t0 + e, N)];
+    load_window<1, NT, MAXP>(wb, wrow, T + Rj, false, 0, 1,
+                             [&](int e) { return wrap_mod(t0 + e, N); });
     __syncthreads();
     const int nout = T + Rn;
     double vv[MAXP];

@@ -22,21 +22,20 @@ namespace jwv {
 template <int L, int C, int NT, int CAP, bool FMA>
 __global__ __launch_bounds__(NT) void wpt_fwd_res(const double* __restrict__ src, AxisView sv,
                                                   double* __restrict__ dst, AxisView dv, int n,
-                                                  int nlev, int inner,
+                                                  int nlev, int inner, int dma,
                                                   typename FB<L>::Fwd tp) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   constexpr int MAXP = (CAP / 2 * C + NT - 1) / NT;
+  constexpr int MAXU = (CAP * C + NT - 1) / NT;
   const int ncb = (inner + C - 1) / C;
   const int64_t o = blockIdx.x / ncb;
   const int c0 = (blockIdx.x % ncb) * C;
   const double* s = src + view_base(sv, o) + c0;
   double* y = dst + view_base(dv, o) + c0;
   const int tid = threadIdx.x;
-  for (int q = tid; q < n * C; q += NT) {
-    const int i = q / C, c = q % C;
-    lds[q] = (c0 + c < inner) ? s[(int64_t)i * sv.s_len + c] : 0.0;
-  }
-  __syncthreads();
+  load_window<C, NT, MAXU>(lds, s, n, dma != 0, c0, inner,
+                           [&](int e) { return (int64_t)e * sv.s_len; });
+  dma_fence_barrier();
   const int np = (n >> 1) * C;
   int h = n;
   for (int lev = 0; lev < nlev; ++lev) {
@@ -78,11 +77,13 @@ __global__ __launch_bounds__(NT) void wpt_fwd_res(const double* __restrict__ src
 template <int L, int C, int NT, int T, int KMAX, bool FMA>
 __global__ __launch_bounds__(NT) void wpt_fwd_tile(const double* __restrict__ src, AxisView sv,
                                                    double* __restrict__ dst, AxisView dv, int h,
-                                                   int K, int inner, typename FB<L>::Fwd tp) {
+                                                   int K, int inner, int dma,
+                                                   typename FB<L>::Fwd tp) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   constexpr int LM = LMax<L>::v;
   constexpr int M0MAX = T + (LM - 2) * ((1 << KMAX) - 1);
   constexpr int MAXP = ((M0MAX - (LM - 2)) / 2 * C + NT - 1) / NT;
+  constexpr int MAXU = (M0MAX * C + NT - 1) / NT;
   const int nL = FB<L>::n(tp);
   const int ntile = h / T;
   const int ncb = (inner + C - 1) / C;
@@ -99,11 +100,9 @@ __global__ __launch_bounds__(NT) void wpt_fwd_tile(const double* __restrict__ sr
 
   const int m0 = T + (nL - 2) * ((1 << K) - 1);
   const int msk = h - 1;
-  for (int q = tid; q < m0 * C; q += NT) {
-    const int e = q / C, c = q % C;
-    lds[q] = (c0 + c < inner) ? s[(int64_t)((t * T + e) & msk) * sv.s_len + c] : 0.0;
-  }
-  __syncthreads();
+  load_window<C, NT, MAXU>(lds, s, m0, dma != 0, c0, inner,
+                           [&](int e) { return (int64_t)((t * T + e) & msk) * sv.s_len; });
+  dma_fence_barrier();
   int m = m0;
   for (int l = 1; l <= K; ++l) {
     const int mo = (m - (nL - 2)) >> 1;
@@ -151,10 +150,11 @@ __global__ __launch_bounds__(NT) void wpt_fwd_tile(const double* __restrict__ sr
 template <int L, int C, int NT, int CAP, bool FMA>
 __global__ __launch_bounds__(NT) void wpt_rev_res(const double* __restrict__ src, AxisView sv,
                                                   double* __restrict__ dst, AxisView dv, int n,
-                                                  int h0, int nlev, int inner,
+                                                  int h0, int nlev, int inner, int dma,
                                                   typename FB<L>::Rev tp) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   constexpr int MAXP = (CAP / 2 * C + NT - 1) / NT;
+  constexpr int MAXU = (CAP * C + NT - 1) / NT;
   const int nL = FB<L>::nr(tp);
   const int ncb = (inner + C - 1) / C;
   const int64_t o = blockIdx.x / ncb;
@@ -162,11 +162,9 @@ __global__ __launch_bounds__(NT) void wpt_rev_res(const double* __restrict__ src
   const double* s = src + view_base(sv, o) + c0;
   double* y = dst + view_base(dv, o) + c0;
   const int tid = threadIdx.x;
-  for (int q = tid; q < n * C; q += NT) {
-    const int i = q / C, c = q % C;
-    lds[q] = (c0 + c < inner) ? s[(int64_t)i * sv.s_len + c] : 0.0;
-  }
-  __syncthreads();
+  load_window<C, NT, MAXU>(lds, s, n, dma != 0, c0, inner,
+                           [&](int e) { return (int64_t)e * sv.s_len; });
+  dma_fence_barrier();
   const int np = (n >> 1) * C;
   int h = h0;
   for (int lev = 0; lev < nlev; ++lev) {
@@ -217,11 +215,13 @@ __global__ __launch_bounds__(NT) void wpt_rev_res(const double* __restrict__ src
 template <int L, int C, int NT, int T, int KMAX, bool FMA>
 __global__ __launch_bounds__(NT) void wpt_rev_tile(const double* __restrict__ src, AxisView sv,
                                                    double* __restrict__ dst, AxisView dv, int hK,
-                                                   int K, int inner, typename FB<L>::Rev tp) {
+                                                   int K, int inner, int dma,
+                                                   typename FB<L>::Rev tp) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   constexpr int LM = LMax<L>::v;
   constexpr int QM = (LM + 1) / 2;
   constexpr int MAXP = ((T / 2 + (1 << KMAX) * (QM + 2)) * C + NT - 1) / NT;
+  constexpr int MAXU = ((T + (1 << KMAX) * (2 * QM + 4)) * C + NT - 1) / NT;
   const int nL = FB<L>::nr(tp);
   const int Q = (nL + 1) >> 1;
   const int ntile = hK / T;
@@ -246,15 +246,13 @@ __global__ __launch_bounds__(NT) void wpt_rev_tile(const double* __restrict__ sr
   {  // coarsest level: 2^K band windows
     const int BK = win_b(K), WK = win_e(K) - BK;
     const int band = hK >> K, bm = band - 1, nb = 1 << K;
-    for (int q = tid; q < nb * WK * C; q += NT) {
-      const int pr = q / C, c = q % C;
-      const int f = pr / WK, e = pr % WK;
-      lds[q] = (c0 + c < inner)
-                   ? s[((int64_t)f * band + ((BK + e) & bm)) * sv.s_len + c]
-                   : 0.0;
-    }
+    // the 2^K band windows, stacked: row e' = f*WK + e  (WK is even)
+    load_window<C, NT, MAXU>(lds, s, nb * WK, dma != 0, c0, inner, [&](int r) {
+      const int f = r / WK, e = r % WK;
+      return ((int64_t)f * band + ((BK + e) & bm)) * sv.s_len;
+    });
   }
-  __syncthreads();
+  dma_fence_barrier();
   for (int l = K - 1; l >= 0; --l) {
     const int half = hK >> (l + 1), hm = half - 1;
     const int Bl = win_b(l), Bl1 = win_b(l + 1);
