@@ -95,6 +95,8 @@ typedef struct jwv_kernel_stat {
 } jwv_kernel_stat;
 int jwv_ctx_profile_enable(jwv_ctx* ctx, int on);
 int jwv_ctx_profile_read(jwv_ctx* ctx, jwv_kernel_stat* out, int max_out, int* n_out);
+/* Restrict profiling events to one kernel kind (by name; NULL or "" = all). */
+int jwv_ctx_profile_select(jwv_ctx* ctx, const char* kind);
 /* Release cached device workspace. */
 int jwv_ctx_trim(jwv_ctx* ctx);
 int jwv_version(void);

@@ -59,6 +59,7 @@ _SIGS = {
     "jwv_ctx_synchronize": [_CTX],
     "jwv_ctx_trim": [_CTX],
     "jwv_ctx_profile_enable": [_CTX, _int],
+    "jwv_ctx_profile_select": [_CTX, ctypes.c_char_p],
     "jwv_ctx_profile_read": [_CTX, ctypes.POINTER(KernelStat), _int, ctypes.POINTER(_int)],
     "jwv_modwt_filters": [_TP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)],
 }

@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -53,6 +54,7 @@ struct jwv_ctx {
   DevBuf hin, hout;  // staging for the host-pointer entry points
   // profiling: hipEvent pairs around every kernel launch on the launch stream
   bool prof = false;
+  int prof_only = -1;  // -1: every kind; else one KernelKind
   struct Rec { int kind; double bytes; hipEvent_t e0, e1; };
   std::vector<Rec> recs;
   std::vector<hipEvent_t> ev_pool;
@@ -166,7 +168,8 @@ struct ProfScope {
   jwv_ctx* c;
   bool on;
   size_t idx = 0;
-  ProfScope(jwv_ctx* c_, int kind, double bytes) : c(c_), on(c_->prof) {
+  ProfScope(jwv_ctx* c_, int kind, double bytes)
+      : c(c_), on(c_->prof && (c_->prof_only < 0 || c_->prof_only == kind)) {
     if (!on) return;
     jwv_ctx::Rec r{kind, bytes, take_event(c), take_event(c)};
     hipchk(hipEventRecord(r.e0, c->stream), "hipEventRecord");
@@ -636,6 +639,34 @@ void need_device_ptrs(const double* x, const double* y) { check_ptrs(x, y); }
 
 // dispatch shims for the two math modes
 namespace jwv {
+static int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v ? std::atoi(v) : dflt;
+}
+int Geo::fwd_t1() {
+  static const int t = env_int("JWV_FWD_T", kFwtT1) == 2048 ? 2048 : kFwtT1;
+  return t;
+}
+int Geo::rev_t1() {
+  static const int t = env_int("JWV_REV_T", kFwtT1) == 2048 ? 2048 : kFwtT1;
+  return t;
+}
+bool Geo::fwd_stream() {
+  static const bool p = env_int("JWV_FWD_STREAM", 0) != 0;
+  return p;
+}
+int Geo::stream_blocks_per_cu() {
+  static const int n = env_int("JWV_STREAM_BPC", 2);
+  return n < 1 ? 1 : (n > 8 ? 8 : n);
+}
+int Geo::stream_ntc() {
+  static const int n = env_int("JWV_STREAM_NTC", 512) == 256 ? 256 : 512;
+  return n;
+}
+bool Geo::rev_pref() {
+  static const bool p = env_int("JWV_REV_PREF", 0) != 0;
+  return p;
+}
 #define JWV_MODE2(name, ...) \
   return fma ? fused::name(__VA_ARGS__) : exact::name(__VA_ARGS__)
 hipError_t launch_fwt_fwd_res(const Bank& b, bool fma, int C, const ResArgs& a, hipStream_t s) {
@@ -747,6 +778,18 @@ int jwv_ctx_profile_enable(jwv_ctx* c, int on) {
   if (!c) return set_err(nullptr, JWV_ERR_BAD_CALL, "jwv_ctx is NULL");
   std::lock_guard<std::mutex> lk(c->mu);
   c->prof = on != 0;
+  return JWV_OK;
+}
+
+int jwv_ctx_profile_select(jwv_ctx* c, const char* kind) {
+  if (!c) return set_err(nullptr, JWV_ERR_BAD_CALL, "jwv_ctx is NULL");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->prof_only = -1;
+  if (kind && *kind) {
+    for (int k = 0; k < K_NKINDS; ++k)
+      if (std::strcmp(kind, kKindNames[k]) == 0) c->prof_only = k;
+    if (c->prof_only < 0) return set_err(c, JWV_ERR_BAD_CALL, std::string("unknown kernel kind ") + kind);
+  }
   return JWV_OK;
 }
 

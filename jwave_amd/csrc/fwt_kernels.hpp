@@ -94,53 +94,80 @@ __device__ __forceinline__ void fwd_pair(const typename FB<L>::Fwd& tp, At at, d
 // non-wrapped terms (q <= mg) in q-descending order first, then the wrapped
 // ones (q > mg) in q-descending order.  Valid for h >= L (at most one wrap);
 // smaller levels use rev_level_small.  A(q)/D(q) return a[m-q], d[m-q].
-template <int L, bool FMA, typename GetA, typename GetD>
-__device__ __forceinline__ void rev_pair(const typename FB<L>::Rev& tp, int mg, GetA A, GetD D,
-                                         double& xe, double& xo) {
-  constexpr int LM = LMax<L>::v;
-  constexpr int QM = (LM + 1) / 2;
+// Array-head case of rev_pair (mg < Q-1, only the first pairs of a level):
+// non-wrapped terms (q <= mg) q-descending, then wrapped ones (q > mg).
+// Kept out of line so the unrolled interior loops stay small.  A/D point at
+// a[m], d[m] (stride `st`), so term q reads A[-q*st].
+// A(q), D(q) return a[m-q], d[m-q] (wrapped by the caller).  Inlined with
+// static tap indices (a call would need a stack frame = scratch).
+template <int L, bool FMA, typename GA, typename GD>
+__device__ __forceinline__ void rev_pair_head(const typename FB<L>::Rev& tp, int mg, GA A, GD D,
+                                              double& xe, double& xo) {
+  constexpr int QM = (LMax<L>::v + 1) / 2;
   const int nt = FB<L>::nr(tp);
-  const int qe = (nt + 1) >> 1;  // even taps
-  const int qo = nt >> 1;        // odd taps
+  const int qe = (nt + 1) >> 1, qo = nt >> 1;
   double se = 0.0, so = 0.0;
-  auto term_e = [&](int q) {
-    const int j = 2 * q;
-    double t = A(q) * FB<L>::lor(tp, j);
-    t = mac<FMA>(t, D(q), FB<L>::hir(tp, j));
-    return FB<L>::scale(t, tp);
-  };
-  auto term_o = [&](int q) {
-    const int j = 2 * q + 1;
-    double t = A(q) * FB<L>::lor(tp, j);
-    t = mac<FMA>(t, D(q), FB<L>::hir(tp, j));
-    return FB<L>::scale(t, tp);
-  };
-  if (mg >= QM - 1 || (!FB<L>::kStatic && mg >= qe - 1)) {
-    // interior: plain q-descending order
-    if constexpr (FB<L>::kStatic) {
 #pragma unroll
-      for (int q = QM - 1; q >= 0; --q) {
-        if (q < qe) se += term_e(q);
-        if (q < qo) so += term_o(q);
-      }
-    } else {
-      for (int q = qe - 1; q >= 0; --q) {
-        se += term_e(q);
-        if (q < qo) so += term_o(q);
+  for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+    for (int q = QM - 1; q >= 0; --q) {
+      if (q >= qe || (q <= mg) != (pass == 0)) continue;
+      double t = A(q) * FB<L>::lor(tp, 2 * q);
+      t = mac<FMA>(t, D(q), FB<L>::hir(tp, 2 * q));
+      se += FB<L>::scale(t, tp);
+    }
+  }
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+    for (int q = QM - 1; q >= 0; --q) {
+      if (q >= qo || (q <= mg) != (pass == 0)) continue;
+      double t = A(q) * FB<L>::lor(tp, 2 * q + 1);
+      t = mac<FMA>(t, D(q), FB<L>::hir(tp, 2 * q + 1));
+      so += FB<L>::scale(t, tp);
+    }
+  }
+  xe = se;
+  xo = so;
+}
+
+// Outputs x[2m] (even taps j=2q) and x[2m+1] (odd taps j=2q+1) of one
+// synthesis level of size h >= L (at most one wrap).  Term q reads a[m-q],
+// d[m-q] = A[-q*st], D[-q*st] (the caller's window already holds the periodic
+// extension).  Scatter order of Wavelet.reverse = i ascending = q descending
+// for interior pairs (mg >= Q-1, checked by the caller: head pairs go to
+// rev_pair_head).
+template <int L, bool FMA>
+__device__ __forceinline__ void rev_pair(const typename FB<L>::Rev& tp, const double* A,
+                                         const double* D, int st, double& xe, double& xo) {
+  const int nt = FB<L>::nr(tp);
+  const int qe = (nt + 1) >> 1;
+  double se = 0.0, so = 0.0;
+  if constexpr (FB<L>::kStatic) {
+    constexpr int QE = (L + 1) / 2, QO = L / 2;
+#pragma unroll
+    for (int q = QE - 1; q >= 0; --q) {
+      const double a = A[-q * st], d = D[-q * st];
+      double t = a * FB<L>::lor(tp, 2 * q);
+      se += mac<FMA>(t, d, FB<L>::hir(tp, 2 * q));
+      if (q < QO) {
+        double u = a * FB<L>::lor(tp, 2 * q + 1);
+        so += mac<FMA>(u, d, FB<L>::hir(tp, 2 * q + 1));
       }
     }
   } else {
-    // array head: non-wrapped (q <= mg) first, then wrapped (q > mg)
-    for (int q = qe - 1; q >= 0; --q)
-      if (q <= mg) se += term_e(q);
-    for (int q = qe - 1; q >= 0; --q)
-      if (q > mg) se += term_e(q);
-    for (int q = qo - 1; q >= 0; --q)
-      if (q <= mg) so += term_o(q);
-    for (int q = qo - 1; q >= 0; --q)
-      if (q > mg) so += term_o(q);
+    const int qo = nt >> 1;
+    for (int q = qe - 1; q >= 0; --q) {
+      const double a = A[-q * st], d = D[-q * st];
+      double t = a * FB<L>::lor(tp, 2 * q);
+      se += FB<L>::scale(mac<FMA>(t, d, FB<L>::hir(tp, 2 * q)), tp);
+      if (q < qo) {
+        double u = a * FB<L>::lor(tp, 2 * q + 1);
+        so += FB<L>::scale(mac<FMA>(u, d, FB<L>::hir(tp, 2 * q + 1)), tp);
+      }
+    }
   }
-  xe = se;  // se started at +0.0 like arrTime[k] (Wavelet.java:282)
+  xe = se;  // started at +0.0 like arrTime[k] (Wavelet.java:282)
   xo = so;
 }
 
@@ -165,7 +192,9 @@ __device__ double rev_small(const typename FB<L>::Rev& tp, const double* a, cons
 // Forward, resident.  Grid: one block per (outer o, column slab cb).
 // src: level input of length h0 (view sv); dst: coefficient array (view dv):
 // level of size h writes details to dst[h/2 .. h), the final approximation to
-// dst[0 .. h_end).  nlev >= 0 levels; LDS = h0*C doubles.
+// dst[0 .. h_end).  nlev >= 0 levels; LDS = h0*C doubles.  Levels with more
+// than 64 pairs run block-wide; the rest run on wave 0 alone (no block
+// barriers: a deep tail is latency-bound).
 // ====================================================================
 template <int L, int C, int NT, int CAP, bool FMA>
 __global__ __launch_bounds__(NT) void fwt_fwd_res(const double* __restrict__ src, AxisView sv,
@@ -181,39 +210,56 @@ __global__ __launch_bounds__(NT) void fwt_fwd_res(const double* __restrict__ src
   const double* s = src + view_base(sv, o) + c0;
   double* y = dst + view_base(dv, o) + c0;
   const int tid = threadIdx.x;
-
+  JWV_STAMP(0);
   load_window<C, NT, MAXU>(lds, s, h0, dma != 0, c0, inner,
                            [&](int e) { return (int64_t)e * sv.s_len; });
   dma_fence_barrier();
+  JWV_STAMP(1);
 
-  int h = h0;
-  for (int lev = 0; lev < nlev; ++lev) {
+  int h = h0, lev = 0;
+  for (; lev < nlev && (h >> 1) * C > 64; ++lev, h >>= 1) {
+    JWV_STAMP(2 + lev);
     const int half = h >> 1, np = half * C, msk = h - 1;
     double av[MAXP];
-#pragma unroll
-    for (int r = 0; r < MAXP; ++r) {
-      const int p = tid + r * NT;
-      if (p < np) {
+    for_pairs<MAXP, NT>(np, [&](int r, int p, bool v) {
+      const int i = p / C, c = p % C;
+      double a, d;
+      fwd_pair<L, FMA>(tp, [&](int j) { return lds[((2 * i + j) & msk) * C + c]; }, a, d);
+      av[r] = a;
+      if (v && c0 + c < inner) y[(int64_t)(half + i) * dv.s_len + c] = d;
+    });
+    __syncthreads();
+    for_pairs<MAXP, NT>(np, [&](int r, int p, bool v) {
+      if (v) lds[p] = av[r];
+    });
+    __syncthreads();
+  }
+  if (lev < nlev) {  // small levels: wave 0 only
+    if (tid < 64) {
+      int hh = h;
+      for (int lv = lev; lv < nlev; ++lv, hh >>= 1) {
+        const int half = hh >> 1, np = half * C, msk = hh - 1;
+        const bool v = tid < np;
+        const int p = v ? tid : np - 1;
         const int i = p / C, c = p % C;
         double a, d;
         fwd_pair<L, FMA>(tp, [&](int j) { return lds[((2 * i + j) & msk) * C + c]; }, a, d);
-        av[r] = a;
-        if (c0 + c < inner) y[(int64_t)(half + i) * dv.s_len + c] = d;
+        if (v && c0 + c < inner) y[(int64_t)(half + i) * dv.s_len + c] = d;
+        wave_lds_sync();
+        if (v) lds[p] = a;
+        wave_lds_sync();
       }
     }
+    h >>= (nlev - lev);
+    JWV_STAMP(40);
     __syncthreads();
-#pragma unroll
-    for (int r = 0; r < MAXP; ++r) {
-      const int p = tid + r * NT;
-      if (p < np) lds[p] = av[r];
-    }
-    __syncthreads();
-    h = half;
   }
+  JWV_STAMP(41);
   for (int q = tid; q < h * C; q += NT) {
     const int i = q / C, c = q % C;
     if (c0 + c < inner) y[(int64_t)i * dv.s_len + c] = lds[q];
   }
+  JWV_STAMP(42);
 }
 
 // ====================================================================
@@ -266,23 +312,17 @@ __global__ __launch_bounds__(NT) void fwt_fwd_tile(const double* __restrict__ sr
     const int np = mo * C;
     const int64_t dbase = (int64_t)(hl >> 1) + (int64_t)t * own;
     double av[MAXP];
-#pragma unroll
-    for (int r = 0; r < MAXP; ++r) {
-      const int p = tid + r * NT;
-      if (p < np) {
-        const int i = p / C, c = p % C;
-        double a, d;
-        fwd_pair<L, FMA>(tp, [&](int j) { return lds[(2 * i + j) * C + c]; }, a, d);
-        av[r] = a;
-        if (i < own && c0 + c < inner) y[(dbase + i) * dv.s_len + c] = d;
-      }
-    }
+    for_pairs<MAXP, NT>(np, [&](int r, int p, bool v) {
+      const int i = p / C, c = p % C;
+      double a, d;
+      fwd_pair<L, FMA>(tp, [&](int j) { return lds[(2 * i + j) * C + c]; }, a, d);
+      av[r] = a;
+      if (v && i < own && c0 + c < inner) y[(dbase + i) * dv.s_len + c] = d;
+    });
     __syncthreads();
-#pragma unroll
-    for (int r = 0; r < MAXP; ++r) {
-      const int p = tid + r * NT;
-      if (p < np) lds[p] = av[r];
-    }
+    for_pairs<MAXP, NT>(np, [&](int r, int p, bool v) {
+      if (v) lds[p] = av[r];
+    });
     __syncthreads();
     m = mo;
     hl >>= 1;
@@ -295,9 +335,130 @@ __global__ __launch_bounds__(NT) void fwt_fwd_tile(const double* __restrict__ sr
 }
 
 // ====================================================================
+// Forward, streaming (C = 1 hot path: long 1-D signals, batches of them).
+// Persistent blocks of NTC compute threads + 1 loader wave.  The loader wave
+// keeps one tile ahead: while the compute waves run the K fused levels of
+// tile i out of LDS buffer i&1, it LDS-DMAs tile i+1's window into the other
+// buffer, so the CU's HBM stream never pauses for compute (a plain one-tile
+// block loads, then computes, with its co-resident blocks in the same phase).
+// The loader joins every block barrier and never stores, so its own
+// `s_waitcnt vmcnt(0)` waits for its DMA only.  Tile order is XCD-aware: the
+// blocks of one XCD walk a contiguous chunk of tiles side by side, so a
+// tile's halo is its neighbour's head, already in that XCD's L2.
+// Math and outputs are identical to fwt_fwd_tile.
+// ====================================================================
+template <int L, int NTC, int T, int KMAX, bool FMA>
+__global__ __launch_bounds__(NTC + 64) void fwt_fwd_stream(
+    const double* __restrict__ src, AxisView sv, double* __restrict__ dst, AxisView dv,
+    double* __restrict__ adst, AxisView av_, int h, int K, int64_t ntotal,
+    typename FB<L>::Fwd tp) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  constexpr int LM = LMax<L>::v;
+  constexpr int M0MAX = T + (LM - 2) * ((1 << KMAX) - 1);
+  constexpr int WBUF = (M0MAX + 3) & ~1;  // + DMA overrun, even
+  constexpr int MAXP = ((M0MAX - (LM - 2)) / 2 + NTC - 1) / NTC;
+  const int nL = FB<L>::n(tp);
+  const int ntile = h / T;
+  const int tid = threadIdx.x;
+  const bool loader = tid >= NTC;
+  const int lane = tid & 63;
+  const int m0 = T + (nL - 2) * ((1 << K) - 1);
+  const int msk = h - 1;
+  const int nunits = (m0 + 1) >> 1;
+
+  // XCD-aware tile walk: block b sits on XCD b%8 (speed only, not correctness)
+  const int64_t nb = gridDim.x;
+  const int64_t b = blockIdx.x;
+  int64_t first, stride, count;
+  if ((nb & 7) == 0 && (ntotal & 7) == 0) {
+    const int64_t nper = nb >> 3, chunk = ntotal >> 3;
+    const int64_t x = b & 7, slot = b >> 3;
+    first = x * chunk + slot;
+    stride = nper;
+    count = slot < chunk ? (chunk - slot + nper - 1) / nper : 0;
+  } else {
+    first = b;
+    stride = nb;
+    count = b < ntotal ? (ntotal - b + nb - 1) / nb : 0;
+  }
+
+  auto issue = [&](int64_t g, double* buf) {  // loader wave only
+    const int64_t o = g / ntile;
+    const int t = (int)(g % ntile);
+    const double* s = src + view_base(sv, o);
+    const int base = t * T;
+    for (int u0 = 0; u0 < nunits; u0 += 64) {
+      const int u = u0 + lane;
+      if (u < nunits) dma16_asm((const void*)(s + ((base + 2 * u) & msk)), buf + 2 * u0);
+    }
+  };
+
+  if (loader && count > 0) issue(first, lds);
+  if (loader) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int64_t k = 0; k < count; ++k) {
+    const int64_t g = first + k * stride;
+    double* cur = lds + (k & 1) * WBUF;
+    if (k < 10) JWV_STAMP(3 * k);
+    if (loader && k + 1 < count) issue(g + stride, lds + ((k + 1) & 1) * WBUF);
+    const int64_t o = g / ntile;
+    const int t = (int)(g % ntile);
+    double* y = dst + view_base(dv, o);
+    double* ya = adst + view_base(av_, o);
+    int m = m0, hl = h;
+    for (int l = 1; l <= K; ++l) {
+      const int mo = (m - (nL - 2)) >> 1;
+      const int own = T >> l;
+      const int64_t dbase = (int64_t)(hl >> 1) + (int64_t)t * own;
+      double av[MAXP];
+      if (!loader) {
+        for_pairs<MAXP, NTC>(mo, [&](int r, int p, bool v) {
+          double a, d;
+          fwd_pair<L, FMA>(tp, [&](int j) { return cur[2 * p + j]; }, a, d);
+          av[r] = a;
+          if (v && p < own) y[dbase + p] = d;
+        });
+      }
+      __syncthreads();
+      if (!loader) {
+        for_pairs<MAXP, NTC>(mo, [&](int r, int p, bool v) {
+          if (v) cur[p] = av[r];
+        });
+      }
+      __syncthreads();
+      m = mo;
+      hl >>= 1;
+    }
+    const int own = T >> K;
+    if (!loader)
+      for (int q = tid; q < own; q += NTC) ya[(int64_t)t * own + q] = cur[q];
+    if (k < 10) JWV_STAMP(3 * k + 1);
+    if (loader) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // next buffer landed; this buffer free for the tile after
+    if (k < 10) JWV_STAMP(3 * k + 2);
+  }
+}
+
+// One synthesis pair at global pair index m (m < qe-1: array head, whose
+// terms are summed in scatter order by rev_pair_head).  A/D point at the LDS
+// copies of a[m], d[m] (stride C); Aw(q)/Dw(q) give a[m-q]/d[m-q] wrapped.
+// The interior formula is always evaluated (on a clamped index for head
+// pairs) so that the common path stays branch-free.
+template <int L, bool FMA, typename AW, typename DW>
+__device__ __forceinline__ void rev_pair_any(const typename FB<L>::Rev& tp, int m, int qe,
+                                             const double* A, const double* D, int C,
+                                             AW Aw, DW Dw, double& xe, double& xo) {
+  const int sh = m < qe - 1 ? (qe - 1 - m) : 0;  // clamp for head pairs
+  rev_pair<L, FMA>(tp, A + sh * C, D + sh * C, C, xe, xo);
+  if (sh) rev_pair_head<L, FMA>(tp, m, Aw, Dw, xe, xo);
+}
+
+// ====================================================================
 // Reverse, resident.  src holds the coefficient prefix [0, htop) of each
 // signal (htop = h0 << (nlev-1), or h0 when nlev == 0); levels of size h0,
-// 2h0, .., htop run in LDS; the result [0, htop) goes to dst.
+// 2h0, .., htop run in LDS; the result [0, htop) goes to dst.  Levels with at
+// most 64 pairs (the first ones) run on wave 0 alone.
 // ====================================================================
 template <int L, int C, int NT, int CAP, bool FMA>
 __global__ __launch_bounds__(NT) void fwt_rev_res(const double* __restrict__ src, AxisView sv,
@@ -308,6 +469,7 @@ __global__ __launch_bounds__(NT) void fwt_rev_res(const double* __restrict__ src
   constexpr int MAXP = (CAP / 2 * C + NT - 1) / NT;
   constexpr int MAXU = (CAP * C + NT - 1) / NT;
   const int nL = FB<L>::nr(tp);
+  const int qe = (nL + 1) >> 1;
   const int ncb = (inner + C - 1) / C;
   const int64_t o = blockIdx.x / ncb;
   const int c0 = (blockIdx.x % ncb) * C;
@@ -320,35 +482,58 @@ __global__ __launch_bounds__(NT) void fwt_rev_res(const double* __restrict__ src
                            [&](int e) { return (int64_t)e * sv.s_len; });
   dma_fence_barrier();
 
-  int h = h0;
-  for (int lev = 0; lev < nlev; ++lev) {
-    const int half = h >> 1, np = half * C, hm = half - 1;
-    double xe[MAXP], xo[MAXP];
-    if (h >= nL) {
-#pragma unroll
-      for (int r = 0; r < MAXP; ++r) {
-        const int p = tid + r * NT;
-        if (p < np) {
+  // one synthesis pair of a level of size h >= L, from the LDS level image
+  auto pair_at = [&](int h, int p, double& xe, double& xo) {
+    const int half = h >> 1, hm = half - 1;
+    const int m = p / C, c = p % C;
+    const double* lb = lds + c;
+    rev_pair_any<L, FMA>(
+        tp, m, qe, lb + m * C, lb + (half + m) * C, C,
+        [=](int q) { return lb[((m - q) & hm) * C]; },
+        [=](int q) { return lb[(half + ((m - q) & hm)) * C]; }, xe, xo);
+  };
+  // levels with h < L wrap several times: literal scatter order (one site)
+  auto pair_small = [&](int h, int p, double& xe, double& xo) {
+    const int half = h >> 1;
+    const int m = p / C, c = p % C;
+    const double* lb = lds + c;
+    xe = rev_small<L, FMA>(tp, lb, lb + half * C, C, h, 2 * m);
+    xo = rev_small<L, FMA>(tp, lb, lb + half * C, C, h, 2 * m + 1);
+  };
+
+  int h = h0, lev = 0;
+  if ((h >> 1) * C <= 64 && nlev > 0) {  // small levels: wave 0 only
+    if (tid < 64) {
+      int hh = h;
+      for (int lv = 0; lv < nlev && (hh >> 1) * C <= 64; ++lv, hh <<= 1) {
+        const int np = (hh >> 1) * C;
+        const bool v = tid < np;
+        const int p = v ? tid : np - 1;
+        double xe, xo;
+        if (hh < nL) pair_small(hh, p, xe, xo); else pair_at(hh, p, xe, xo);
+        wave_lds_sync();
+        if (v) {
           const int m = p / C, c = p % C;
-          rev_pair<L, FMA>(
-              tp, m, [&](int q) { return lds[((m - q) & hm) * C + c]; },
-              [&](int q) { return lds[(half + ((m - q) & hm)) * C + c]; }, xe[r], xo[r]);
+          lds[(2 * m) * C + c] = xe;
+          lds[(2 * m + 1) * C + c] = xo;
         }
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < MAXP; ++r) {
-        const int p = tid + r * NT;
-        if (p < np) {
-          const int m = p / C, c = p % C;
-          xe[r] = rev_small<L, FMA>(tp, lds + c, lds + half * C + c, C, h, 2 * m);
-          xo[r] = rev_small<L, FMA>(tp, lds + c, lds + half * C + c, C, h, 2 * m + 1);
-        }
+        wave_lds_sync();
       }
     }
+    while (lev < nlev && (h >> 1) * C <= 64) { ++lev; h <<= 1; }
+    __syncthreads();
+  }
+  // block-wide levels that still wrap several times (runtime L with C = 8:
+  // h < 64 so np <= 256 = 2 slots of NT >= 128; all read before any write)
+  for (; lev < nlev && h < nL; ++lev, h <<= 1) {
+    const int np = (h >> 1) * C;
+    double xe[2] = {0.0, 0.0}, xo[2] = {0.0, 0.0};
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+      if (tid + r * NT < np) pair_small(h, tid + r * NT, xe[r], xo[r]);
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < MAXP; ++r) {
+    for (int r = 0; r < 2; ++r) {
       const int p = tid + r * NT;
       if (p < np) {
         const int m = p / C, c = p % C;
@@ -357,7 +542,20 @@ __global__ __launch_bounds__(NT) void fwt_rev_res(const double* __restrict__ src
       }
     }
     __syncthreads();
-    h <<= 1;
+  }
+  for (; lev < nlev; ++lev, h <<= 1) {
+    const int np = (h >> 1) * C;
+    double xe[MAXP], xo[MAXP];
+    for_pairs<MAXP, NT>(np, [&](int r, int p, bool v) { pair_at(h, p, xe[r], xo[r]); });
+    __syncthreads();
+    for_pairs<MAXP, NT>(np, [&](int r, int p, bool v) {
+      if (v) {
+        const int m = p / C, c = p % C;
+        lds[(2 * m) * C + c] = xe[r];
+        lds[(2 * m + 1) * C + c] = xo[r];
+      }
+    });
+    __syncthreads();
   }
   for (int q = tid; q < htop * C; q += NT) {
     const int i = q / C, c = q % C;
@@ -371,9 +569,12 @@ __global__ __launch_bounds__(NT) void fwt_rev_res(const double* __restrict__ src
 // cv, details of level size h at coef[h/2 .. h)); dst: output of length hK.
 // Tile t produces dst[tT, tT+T).  Windows (pair aligned) from fine to coarse:
 //   B_0 = tT, E_0 = tT+T;  B_{l+1} = even_floor(B_l/2 - (Q-1)), E_{l+1} = E_l/2
-// LDS: A window (<= T/2 + 2Q + 2) then D window (same bound), times C.
+// PREF = false: the detail window of each level is loaded just before that
+// level; LDS = A window (<= T/2 + 2Q + 4) + one D window (same bound).
+// PREF = true: all detail windows are fetched in one burst up front (one
+// memory latency per block); LDS = A window + sum of D windows (<= T + K(2Q+4)).
 // ====================================================================
-template <int L, int C, int NT, int T, int KMAX, bool FMA>
+template <int L, int C, int NT, int T, int KMAX, bool FMA, bool PREF>
 __global__ __launch_bounds__(NT) void fwt_rev_tile(const double* __restrict__ asrc, AxisView as,
                                                    const double* __restrict__ coef, AxisView cv,
                                                    double* __restrict__ dst, AxisView dv, int h1,
@@ -382,9 +583,9 @@ __global__ __launch_bounds__(NT) void fwt_rev_tile(const double* __restrict__ as
   extern __shared__ __attribute__((aligned(16))) double lds[];
   constexpr int LM = LMax<L>::v;
   constexpr int QM = (LM + 1) / 2;
-  constexpr int WMAX = T / 2 + 2 * QM + 4;  // max window (pairs*2) at level >= 1
+  constexpr int WA = T / 2 + 2 * QM + 4;  // window bound (levels >= 1)
   constexpr int MAXP = ((T / 2 + QM + 2) * C + NT - 1) / NT;
-  constexpr int MAXU = (WMAX * C + NT - 1) / NT;
+  constexpr int MAXU = (WA * C + NT - 1) / NT;
   const int nL = FB<L>::nr(tp);
   const int Q = (nL + 1) >> 1;
   const int hK = h1 << (K - 1);
@@ -402,73 +603,85 @@ __global__ __launch_bounds__(NT) void fwt_rev_tile(const double* __restrict__ as
   double* y = dst + view_base(dv, o) + c0;
   const int tid = threadIdx.x;
   double* abuf = lds;
-  double* dbuf = lds + WMAX * C;
+  double* dall = lds + WA * C;
 
-  // window bounds; B may be negative (periodic).  Recomputed on demand so no
-  // runtime-indexed register array is needed.
   auto win_b = [&](int l) {
     int bb = t * T;
     for (int k = 0; k < l; ++k) bb = ((bb >> 1) - (Q - 1)) & ~1;  // even floor
     return bb;
   };
   auto win_e = [&](int l) { return (t * T + T) >> l; };
-  // coarsest approximation window: a of length h1/2 = hK >> K
+  auto load_d = [&](double* buf, int l) {
+    const int half = hK >> (l + 1), hm = half - 1;
+    const int Bl1 = win_b(l + 1);
+    load_window<C, NT, MAXU>(buf, sc, win_e(l + 1) - Bl1, dma != 0, c0, inner, [&](int e) {
+      return ((int64_t)half + ((Bl1 + e) & hm)) * cv.s_len;
+    });
+  };
+
   {
     const int BK = win_b(K);
-    const int W = win_e(K) - BK;
     const int am = (hK >> K) - 1;
-    load_window<C, NT, MAXU>(abuf, sa, W, dma != 0, c0, inner,
+    load_window<C, NT, MAXU>(abuf, sa, win_e(K) - BK, dma != 0, c0, inner,
                              [&](int e) { return (int64_t)((BK + e) & am) * as.s_len; });
   }
+  if constexpr (PREF) {
+    int doff = 0;
+    for (int l = K - 1; l >= 0; --l) {
+      load_d(dall + doff * C, l);
+      doff += win_e(l + 1) - win_b(l + 1);
+    }
+    dma_fence_barrier();
+  }
+  int doff = 0;
   for (int l = K - 1; l >= 0; --l) {
-    // level with output size hl = hK >> l; inputs a,d of length half = hl/2
+    // level with output size hK >> l; inputs a, d of length half
     const int half = hK >> (l + 1), hm = half - 1;
     const int Bl = win_b(l), Bl1 = win_b(l + 1);
     const int Wd = win_e(l + 1) - Bl1;
-    load_window<C, NT, MAXU>(dbuf, sc, Wd, dma != 0, c0, inner, [&](int e) {
-      return ((int64_t)half + ((Bl1 + e) & hm)) * cv.s_len;
-    });
-    dma_fence_barrier();
-    const int pbase = Bl >> 1;                     // first pair (global, may be <0)
-    const int np = ((win_e(l) - Bl) >> 1) * C;     // pairs in window
-    const int off = pbase - Bl1;                   // local index of a[pbase]
-    double xe[MAXP], xo[MAXP];
-#pragma unroll
-    for (int r = 0; r < MAXP; ++r) {
-      const int p = tid + r * NT;
-      if (p < np) {
-        const int ml = p / C, c = p % C;
-        const int mg = (pbase + ml) & hm;
-        const int li = off + ml;
-        rev_pair<L, FMA>(
-            tp, mg, [&](int q) { return abuf[(li - q) * C + c]; },
-            [&](int q) { return dbuf[(li - q) * C + c]; }, xe[r], xo[r]);
-      }
+    const double* dbuf = PREF ? dall + doff * C : dall;
+    doff += Wd;
+    if constexpr (!PREF) {
+      load_d(dall, l);
+      dma_fence_barrier();
     }
-    if (l == 0) {
-#pragma unroll
-      for (int r = 0; r < MAXP; ++r) {
-        const int p = tid + r * NT;
-        if (p < np) {
-          const int ml = p / C, c = p % C;
-          if (c0 + c < inner) {
-            const int64_t k = (int64_t)t * T + 2 * ml;
-            y[k * dv.s_len + c] = xe[r];
-            y[(k + 1) * dv.s_len + c] = xo[r];
-          }
-        }
+    const int pbase = Bl >> 1;                  // first pair (global, may be <0)
+    const int np = ((win_e(l) - Bl) >> 1) * C;  // pairs in window
+    const int off = pbase - Bl1;                // local index of a[pbase]
+    double xe[MAXP], xo[MAXP];
+    for_pairs<MAXP, NT>(np, [&](int r, int p, bool v) {
+      const int ml = p / C, c = p % C;
+      const int mg = (pbase + ml) & hm;
+      const int li = off + ml;
+      const double* ab = abuf + c;
+      const double* db = dbuf + c;
+      // window indices never wrap (the halo holds the periodic extension)
+      if (mg >= Q - 1) {
+        rev_pair<L, FMA>(tp, ab + li * C, db + li * C, C, xe[r], xo[r]);
+      } else {
+        rev_pair_head<L, FMA>(
+            tp, mg, [=](int q) { return ab[(li - q) * C]; },
+            [=](int q) { return db[(li - q) * C]; }, xe[r], xo[r]);
       }
+    });
+    if (l == 0) {
+      for_pairs<MAXP, NT>(np, [&](int r, int p, bool v) {
+        const int ml = p / C, c = p % C;
+        if (v && c0 + c < inner) {
+          const int64_t k = (int64_t)t * T + 2 * ml;
+          y[k * dv.s_len + c] = xe[r];
+          y[(k + 1) * dv.s_len + c] = xo[r];
+        }
+      });
     } else {
       __syncthreads();
-#pragma unroll
-      for (int r = 0; r < MAXP; ++r) {
-        const int p = tid + r * NT;
-        if (p < np) {
+      for_pairs<MAXP, NT>(np, [&](int r, int p, bool v) {
+        if (v) {
           const int ml = p / C, c = p % C;
           abuf[(2 * ml) * C + c] = xe[r];
           abuf[(2 * ml + 1) * C + c] = xo[r];
         }
-      }
+      });
       __syncthreads();
     }
   }

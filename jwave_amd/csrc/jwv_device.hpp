@@ -18,6 +18,24 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Diagnostic phase stamps (separate build with -DJWV_STAMPS only): thread 0
+// of block 0 records s_memrealtime (100 MHz) at numbered points.
+#ifdef JWV_STAMPS
+extern __device__ unsigned long long jwv_stamps[64];
+extern __device__ unsigned long long jwv_clocks[64];
+#define JWV_STAMP(k)                                                        \
+  do {                                                                      \
+    if (threadIdx.x == 0 && blockIdx.x == 0) {                              \
+      jwv_stamps[(k)] = __builtin_amdgcn_s_memrealtime();                   \
+      jwv_clocks[(k)] = __builtin_amdgcn_s_memtime();                       \
+    }                                                                       \
+  } while (0)
+#else
+#define JWV_STAMP(k) \
+  do {               \
+  } while (0)
+#endif
+
 namespace jwv {
 
 constexpr int kMaxTaps = 64;
@@ -57,6 +75,23 @@ struct AnyTaps {
   int32_t L;
   int32_t pad_;
 };
+
+// LDS-DMA of 16 B per lane issued through inline asm: the compiler's waitcnt
+// analysis does not see it, so barriers elsewhere in the kernel do not get a
+// conservative vmcnt(0) (which would make every wave drain its global
+// stores).  The issuing wave must `s_waitcnt vmcnt(0)` itself (asm) before a
+// barrier that publishes the data.  lds_dst must be wave-uniform.
+__device__ __forceinline__ void dma16_asm(const void* g, double* lds_dst) {
+  const unsigned lds_addr =
+      (unsigned)(uintptr_t)((__attribute__((address_space(3))) double*)lds_dst);
+  asm volatile(
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %0, off"
+      :
+      : "v"(g), "s"(lds_addr)
+      : "memory", "m0");
+}
 
 // Wait for this wave's LDS-DMA loads, then a workgroup barrier: after it
 // every wave sees every other wave's DMA'd rows in LDS.
@@ -109,6 +144,42 @@ __device__ __forceinline__ void load_window(double* lds, const double* __restric
     const int q = tid + r * NT;
     if (q < total) lds[q] = v[r];
   }
+}
+
+// Pair-slot iteration for a level with np pairs: slot r of this thread is
+// pair p = tid + r*NT.  f(r, p, valid) must only store when `valid`.
+// When R = ceil(np/NT) <= 4 the slots run branch-free (invalid slots compute
+// on a clamped pair index) so the independent LDS reads / FP64 chains of all
+// slots overlap; larger R keeps the MAXP-unrolled guarded form.
+template <int R, int NT, typename F>
+__device__ __forceinline__ void pairs_flat(int np, F& f) {
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int p0 = (int)threadIdx.x + r * NT;
+    const bool v = p0 < np;
+    f(r, v ? p0 : np - 1, v);
+  }
+}
+template <int MAXP, int NT, typename F>
+__device__ __forceinline__ void for_pairs(int np, F&& f) {
+  const int R = (np + NT - 1) / NT;
+  if (R <= 1) { pairs_flat<1, NT>(np, f); return; }
+  if constexpr (MAXP >= 2) if (R == 2) { pairs_flat<2, NT>(np, f); return; }
+  if constexpr (MAXP >= 3) if (R == 3) { pairs_flat<3, NT>(np, f); return; }
+  if constexpr (MAXP >= 4) if (R == 4) { pairs_flat<4, NT>(np, f); return; }
+#pragma unroll
+  for (int r = 0; r < MAXP; ++r) {
+    const int p0 = (int)threadIdx.x + r * NT;
+    if (p0 < np) f(r, p0, true);
+  }
+}
+
+// Wave-local LDS ordering: a wave's LDS ops execute in program order, so only
+// the compiler has to be kept from moving them across this point.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 template <bool FMA>

@@ -71,6 +71,14 @@ struct Geo {
   static constexpr int kWptT8 = 512, kWptK8 = 3;
   static constexpr int kModT = 4096, kModS = 2048;
   static int res_cap(int C) { return C == 1 ? kResCap1 : kResCap8; }
+  // tile of the C = 1 FWT passes: 4096 (default) or 2048, env JWV_FWD_T / JWV_REV_T;
+  // reverse detail prefetch-all: env JWV_REV_PREF=1
+  static int fwd_t1();
+  static int rev_t1();
+  static bool rev_pref();
+  static bool fwd_stream();          // env JWV_FWD_STREAM (default 0)
+  static int stream_blocks_per_cu(); // env JWV_STREAM_BPC (default 2)
+  static int stream_ntc();           // env JWV_STREAM_NTC: 256 | 512 (default 512)
   static int fwt_t(int C) { return C == 1 ? kFwtT1 : kFwtT8; }
   static int fwt_k(int C) { return C == 1 ? kFwtK1 : kFwtK8; }
   static int wpt_t(int C) { return C == 1 ? kWptT1 : kWptT8; }

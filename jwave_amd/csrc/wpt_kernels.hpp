@@ -179,9 +179,13 @@ __global__ __launch_bounds__(NT) void wpt_rev_res(const double* __restrict__ src
         const double* A = lds + (pk * h) * C + c;
         const double* D = lds + (pk * h + half) * C + c;
         if (h >= nL) {
-          rev_pair<L, FMA>(
-              tp, m, [&](int q) { return A[((m - q) & hm) * C]; },
-              [&](int q) { return D[((m - q) & hm) * C]; }, xe[r], xo[r]);
+          if (m >= ((nL + 1) >> 1) - 1) {
+            rev_pair<L, FMA>(tp, A + m * C, D + m * C, C, xe[r], xo[r]);
+          } else {
+            rev_pair_head<L, FMA>(
+                tp, m, [=](int q) { return A[((m - q) & hm) * C]; },
+                [=](int q) { return D[((m - q) & hm) * C]; }, xe[r], xo[r]);
+          }
         } else {
           xe[r] = rev_small<L, FMA>(tp, A, D, C, h, 2 * m);
           xo[r] = rev_small<L, FMA>(tp, A, D, C, h, 2 * m + 1);
@@ -273,9 +277,13 @@ __global__ __launch_bounds__(NT) void wpt_rev_tile(const double* __restrict__ sr
         const int li = off + ml;
         const double* A = lds + ((2 * f) * Wl1) * C + c;
         const double* D = lds + ((2 * f + 1) * Wl1) * C + c;
-        rev_pair<L, FMA>(
-            tp, mg, [&](int q) { return A[(li - q) * C]; }, [&](int q) { return D[(li - q) * C]; },
-            xe[r], xo[r]);
+        if (mg >= Q - 1) {
+          rev_pair<L, FMA>(tp, A + li * C, D + li * C, C, xe[r], xo[r]);
+        } else {
+          rev_pair_head<L, FMA>(
+              tp, mg, [=](int q) { return A[(li - q) * C]; }, [=](int q) { return D[(li - q) * C]; },
+              xe[r], xo[r]);
+        }
       }
     }
     if (l == 0) {

@@ -71,6 +71,10 @@ class Context:
         """Record hipEvents around every kernel launch (see jwv_ctx_profile_enable)."""
         self._check(self._lib.jwv_ctx_profile_enable(self.handle, 1 if on else 0))
 
+    def profile_select(self, kind=None):
+        """Restrict profiling events to one kernel kind (None = all)."""
+        self._check(self._lib.jwv_ctx_profile_select(self.handle, kind.encode() if kind else None))
+
     def profile_read(self):
         """-> {kind: {"launches", "total_ms", "bytes"}} since the last read (synchronises)."""
         arr = (L.KernelStat * 32)()

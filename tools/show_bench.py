@@ -17,7 +17,7 @@ for f in sorted(glob.glob(os.path.join(d, "bench_*.json"))):
     print("%-26s %.4g samples/s  %.4f ms/step  %7.1f GB/s  dom=%s %.1f us %.0f GB/s (%.1f%%)  err=%.2g"
           % (os.path.basename(f), r["value"], r["ms_per_step"], r["hbm_gbps"], rf["kernel"],
              rf["avg_launch_us"], rf["achieved"], 100 * rf["frac"], r["roundtrip_max_abs_err"]))
-    for k, v in r["kernels"].items():
+    for k, v in r.get("kernels", r.get("kernels_profiled_pass", {})).items():
         print("    %-16s n=%-4d avg %9.2f us  %7.1f GB/s" % (k, v["launches"], v["avg_us"], v["GBps"]))
     if r.get("cpu_baseline"):
         print("    cpu:", r["cpu_baseline"])
