@@ -151,6 +151,22 @@ int jwv_fwt3d_fwd_f64_dev(const double* x, double* y, int64_t p, int64_t q, int6
 int jwv_fwt3d_rev_f64_dev(const double* y, double* x, int64_t p, int64_t q, int64_t r,
                           int lvl_p, int lvl_q, int lvl_r, const jwv_taps* t, jwv_ctx* ctx);
 
+/* ---- one axis of a block -------------------------------------------------------
+ * The per-dimension pass inside BasicTransform's 2-D/3-D loops
+ * (BasicTransform.java:369-395 rows / columns, :520-558 lines along i): the
+ * FWT (or WPT) of every line along the middle axis of a contiguous
+ * [outer][len][inner] block.  Rows: inner = 1; columns of a slab: outer = 1.
+ * Device pointers only; used by the sharded 2-D transform (column pass on a
+ * [rows][cols/W] slab after the all-to-all). */
+int jwv_fwt_axis_fwd_f64_dev(const double* x, double* y, int64_t outer, int64_t len,
+                             int64_t inner, int level, const jwv_taps* t, jwv_ctx* ctx);
+int jwv_fwt_axis_rev_f64_dev(const double* y, double* x, int64_t outer, int64_t len,
+                             int64_t inner, int level, const jwv_taps* t, jwv_ctx* ctx);
+int jwv_wpt_axis_fwd_f64_dev(const double* x, double* y, int64_t outer, int64_t len,
+                             int64_t inner, int level, const jwv_taps* t, jwv_ctx* ctx);
+int jwv_wpt_axis_rev_f64_dev(const double* y, double* x, int64_t outer, int64_t len,
+                             int64_t inner, int level, const jwv_taps* t, jwv_ctx* ctx);
+
 /* ---- WPT ---------------------------------------------------------------------
  * WaveletPacketTransform.forward(double[], int level)  WaveletPacketTransform.java:73-124
  * WaveletPacketTransform.reverse(double[], int level)  WaveletPacketTransform.java:141-191

@@ -1,0 +1,106 @@
+/*
+ * HipFastWaveletTransform — FastWaveletTransform whose per-level loops
+ * (FastWaveletTransform.java:71-153) and the 2-D/3-D loops inherited from
+ * BasicTransform (BasicTransform.java:361-474, 509-659) run as single calls
+ * into libjwave_hip.so.  Drop-in: new Transform( new HipFastWaveletTransform( w ) ).
+ * Wavelets the native path does not reproduce fall back to the Java code.
+ */
+package jwave.amd;
+
+import jwave.exceptions.JWaveException;
+import jwave.transforms.FastWaveletTransform;
+import jwave.transforms.wavelets.Wavelet;
+
+public class HipFastWaveletTransform extends FastWaveletTransform {
+
+  protected final HipNative.Taps _taps;
+  protected final int _kind;
+
+  public HipFastWaveletTransform( Wavelet wavelet ) { this( wavelet, 0 ); }
+
+  protected HipFastWaveletTransform( Wavelet wavelet, int kind ) {
+    super( wavelet );
+    _taps = HipNative.tapsFor( wavelet );
+    _kind = kind;
+  }
+
+  protected double[ ] superForward( double[ ] a, int level ) throws JWaveException {
+    return super.forward( a, level );
+  }
+
+  protected double[ ] superReverse( double[ ] a, int level ) throws JWaveException {
+    return super.reverse( a, level );
+  }
+
+  @Override public double[ ] forward( double[ ] arrTime, int level ) throws JWaveException {
+    if( _taps == null )
+      return superForward( arrTime, level );
+    double[ ] out = new double[ arrTime.length ];
+    HipNative.check( HipNative.t1( _kind, true, arrTime, out, level, _taps ) );
+    return out;
+  }
+
+  @Override public double[ ] reverse( double[ ] arrHilb, int level ) throws JWaveException {
+    if( _taps == null )
+      return superReverse( arrHilb, level );
+    double[ ] out = new double[ arrHilb.length ];
+    HipNative.check( HipNative.t1( _kind, false, arrHilb, out, level, _taps ) );
+    return out;
+  }
+
+  @Override public double[ ][ ] forward( double[ ][ ] m, int lvlM, int lvlN )
+      throws JWaveException {
+    if( _taps == null )
+      return super.forward( m, lvlM, lvlN );
+    return run2d( true, m, lvlM, lvlN );
+  }
+
+  @Override public double[ ][ ] reverse( double[ ][ ] m, int lvlM, int lvlN )
+      throws JWaveException {
+    if( _taps == null )
+      return super.reverse( m, lvlM, lvlN );
+    return run2d( false, m, lvlM, lvlN );
+  }
+
+  private double[ ][ ] run2d( boolean fwd, double[ ][ ] m, int lvlM, int lvlN )
+      throws JWaveException {
+    int rows = m.length, cols = rows == 0 ? 0 : m[ 0 ].length;
+    double[ ] x = HipNative.pack( m ), y = new double[ x.length ];
+    HipNative.Taps t = _taps;
+    HipNative.check( HipNative.transform2d( HipNative.ctx( ), _kind, fwd, x, y, rows, cols, lvlM,
+        lvlN, t.L, t.tw, t.scale, t.lo, t.hi, t.loR, t.hiR ) );
+    return HipNative.unpack( y, rows, cols );
+  }
+
+  @Override public double[ ][ ][ ] forward( double[ ][ ][ ] s, int lvlP, int lvlQ, int lvlR )
+      throws JWaveException {
+    if( _taps == null )
+      return super.forward( s, lvlP, lvlQ, lvlR );
+    return run3d( true, s, lvlP, lvlQ, lvlR );
+  }
+
+  @Override public double[ ][ ][ ] reverse( double[ ][ ][ ] s, int lvlP, int lvlQ, int lvlR )
+      throws JWaveException {
+    if( _taps == null )
+      return super.reverse( s, lvlP, lvlQ, lvlR );
+    return run3d( false, s, lvlP, lvlQ, lvlR );
+  }
+
+  private double[ ][ ][ ] run3d( boolean fwd, double[ ][ ][ ] s, int lp, int lq, int lr )
+      throws JWaveException {
+    int P = s.length, Q = P == 0 ? 0 : s[ 0 ].length, R = Q == 0 ? 0 : s[ 0 ][ 0 ].length;
+    double[ ] x = new double[ P * Q * R ];
+    for( int i = 0; i < P; i++ )
+      for( int j = 0; j < Q; j++ )
+        System.arraycopy( s[ i ][ j ], 0, x, ( i * Q + j ) * R, R );
+    double[ ] y = new double[ x.length ];
+    HipNative.Taps t = _taps;
+    HipNative.check( HipNative.transform3d( HipNative.ctx( ), _kind, fwd, x, y, P, Q, R, lp, lq,
+        lr, t.L, t.tw, t.scale, t.lo, t.hi, t.loR, t.hiR ) );
+    double[ ][ ][ ] out = new double[ P ][ Q ][ R ];
+    for( int i = 0; i < P; i++ )
+      for( int j = 0; j < Q; j++ )
+        System.arraycopy( y, ( i * Q + j ) * R, out[ i ][ j ], 0, R );
+    return out;
+  }
+}

@@ -1,0 +1,137 @@
+/*
+ * HipNative — JNI entry points of libjwave_hip_jni.so (java/native/jwave_hip_jni.c),
+ * a thin shim over the C ABI of libjwave_hip.so (include/jwave_hip.h).
+ *
+ * Source-only in this repository: the build image has no JDK (DESIGN.md §3).
+ */
+package jwave.amd;
+
+import jwave.exceptions.JWaveError;
+import jwave.exceptions.JWaveException;
+import jwave.exceptions.JWaveFailure;
+import jwave.transforms.wavelets.Wavelet;
+import jwave.transforms.wavelets.biorthogonal.BiOrthogonal;
+import jwave.transforms.wavelets.haar.Haar1Orthogonal;
+
+public final class HipNative {
+
+  static { System.loadLibrary( "jwave_hip_jni" ); }
+
+  private HipNative( ) { }
+
+  // status codes of include/jwave_hip.h
+  static final int OK = 0, FAILURE = 1, ILLEGAL_ARGUMENT = 2, DEVICE = 3, BAD_CALL = 4;
+
+  // one jwv_ctx per Java thread (the C ABI serialises per context; the
+  // reference transforms are used concurrently: ParallelTransform.java:258-270)
+  private static final ThreadLocal< Long > CTX = ThreadLocal.withInitial( ( ) -> {
+    long[ ] h = new long[ 1 ];
+    int rc = ctxCreate( Integer.getInteger( "jwave.hip.device", 0 ), h );
+    if( rc != OK )
+      throw new IllegalStateException( lastError( 0L ) );
+    return h[ 0 ];
+  } );
+
+  static long ctx( ) { return CTX.get( ); }
+
+  /** Filter bank as passed to every call: {L, tw, scale} + 4 tap arrays. */
+  static final class Taps {
+    final int L, tw;
+    final double scale;
+    final double[ ] lo, hi, loR, hiR;
+
+    Taps( Wavelet w, double scale ) {
+      L = w.getMotherWavelength( );
+      tw = w.getTransformWavelength( );
+      lo = w.getScalingDeComposition( );
+      hi = w.getWaveletDeComposition( );
+      loR = w.getScalingReConstruction( );
+      hiR = w.getWaveletReConstruction( );
+      this.scale = scale;
+    }
+  }
+
+  /**
+   * The bank for wavelets the native path reproduces bit for bit, or null
+   * (caller then runs the inherited Java code): classes that keep
+   * Wavelet.forward/reverse (Wavelet.java:236-303), the BiOrthogonal family
+   * (same math, BiOrthogonal.java:74-133) and Haar1Orthogonal (reverse x0.5,
+   * Haar1Orthogonal.java:175-207).
+   */
+  static Taps tapsFor( Wavelet w ) {
+    if( w == null || w.getMotherWavelength( ) > 64 )
+      return null;
+    if( w instanceof Haar1Orthogonal )
+      return new Taps( w, 0.5 );
+    if( w instanceof BiOrthogonal )
+      return new Taps( w, 1.0 );
+    try {
+      Class< ? > f = w.getClass( ).getMethod( "forward", double[ ].class, int.class )
+          .getDeclaringClass( );
+      Class< ? > r = w.getClass( ).getMethod( "reverse", double[ ].class, int.class )
+          .getDeclaringClass( );
+      return ( f == Wavelet.class && r == Wavelet.class ) ? new Taps( w, 1.0 ) : null;
+    } catch( NoSuchMethodException e ) {
+      return null;
+    }
+  }
+
+  /** Status -> the reference's exception types (SURVEY §8b). */
+  static void check( int rc ) throws JWaveException {
+    if( rc == OK )
+      return;
+    String msg = lastError( ctx( ) );
+    switch( rc ) {
+      case FAILURE:          throw new JWaveFailure( msg );
+      case ILLEGAL_ARGUMENT: throw new IllegalArgumentException( msg );
+      default:               throw new JWaveError( msg );
+    }
+  }
+
+  // ---- natives (java/native/jwave_hip_jni.c) -------------------------------
+  static native int ctxCreate( int device, long[ ] out );
+  static native String lastError( long ctx );
+
+  /** kind: 0 = FWT, 1 = WPT.  x and y are distinct arrays of length n. */
+  static native int transform1d( long ctx, int kind, boolean forward, double[ ] x, double[ ] y,
+      int level, int L, int tw, double scale, double[ ] lo, double[ ] hi, double[ ] loR,
+      double[ ] hiR );
+
+  /** batch signals of length n, packed contiguously (ld = n). */
+  static native int transformBatch( long ctx, int kind, boolean forward, double[ ] x,
+      double[ ] y, int batch, int n, int level, int L, int tw, double scale, double[ ] lo,
+      double[ ] hi, double[ ] loR, double[ ] hiR );
+
+  /** Rows packed contiguously (rows*cols) by the caller. */
+  static native int transform2d( long ctx, int kind, boolean forward, double[ ] x, double[ ] y,
+      int rows, int cols, int lvlM, int lvlN, int L, int tw, double scale, double[ ] lo,
+      double[ ] hi, double[ ] loR, double[ ] hiR );
+
+  static native int transform3d( long ctx, int kind, boolean forward, double[ ] x, double[ ] y,
+      int p, int q, int r, int lvlP, int lvlQ, int lvlR, int L, int tw, double scale,
+      double[ ] lo, double[ ] hi, double[ ] loR, double[ ] hiR );
+
+  /** wv = (J+1)*n doubles, rows W_1..W_J, V_J. */
+  static native int modwt( long ctx, boolean forward, double[ ] x, double[ ] wv, int n, int J,
+      int L, int tw, double[ ] lo, double[ ] hi, double[ ] loR, double[ ] hiR );
+
+  static int t1( int kind, boolean fwd, double[ ] x, double[ ] y, int level, Taps t ) {
+    return transform1d( ctx( ), kind, fwd, x, y, level, t.L, t.tw, t.scale, t.lo, t.hi, t.loR,
+        t.hiR );
+  }
+
+  static double[ ] pack( double[ ][ ] m ) {
+    int rows = m.length, cols = rows == 0 ? 0 : m[ 0 ].length;
+    double[ ] out = new double[ rows * cols ];
+    for( int i = 0; i < rows; i++ )
+      System.arraycopy( m[ i ], 0, out, i * cols, cols );
+    return out;
+  }
+
+  static double[ ][ ] unpack( double[ ] a, int rows, int cols ) {
+    double[ ][ ] m = new double[ rows ][ cols ];
+    for( int i = 0; i < rows; i++ )
+      System.arraycopy( a, i * cols, m[ i ], 0, cols );
+    return m;
+  }
+}

@@ -1,0 +1,60 @@
+/*
+ * HipWaveletPacketTransform — WaveletPacketTransform (WaveletPacketTransform.java:73-191)
+ * on libjwave_hip.so, plus a batched entry for many signals in one call.
+ */
+package jwave.amd;
+
+import jwave.exceptions.JWaveException;
+import jwave.transforms.WaveletPacketTransform;
+import jwave.transforms.wavelets.Wavelet;
+
+public class HipWaveletPacketTransform extends WaveletPacketTransform {
+
+  private final HipNative.Taps _taps;
+
+  public HipWaveletPacketTransform( Wavelet wavelet ) {
+    super( wavelet );
+    _taps = HipNative.tapsFor( wavelet );
+  }
+
+  @Override public double[ ] forward( double[ ] a, int level ) throws JWaveException {
+    if( _taps == null )
+      return super.forward( a, level );
+    double[ ] out = new double[ a.length ];
+    HipNative.check( HipNative.t1( 1, true, a, out, level, _taps ) );
+    return out;
+  }
+
+  @Override public double[ ] reverse( double[ ] a, int level ) throws JWaveException {
+    if( _taps == null )
+      return super.reverse( a, level );
+    double[ ] out = new double[ a.length ];
+    HipNative.check( HipNative.t1( 1, false, a, out, level, _taps ) );
+    return out;
+  }
+
+  /** Every row (one signal each, equal lengths) with the same level: one
+   *  native call instead of one per signal. */
+  public double[ ][ ] forwardBatch( double[ ][ ] signals, int level ) throws JWaveException {
+    return batch( true, signals, level );
+  }
+
+  public double[ ][ ] reverseBatch( double[ ][ ] coeffs, int level ) throws JWaveException {
+    return batch( false, coeffs, level );
+  }
+
+  private double[ ][ ] batch( boolean fwd, double[ ][ ] m, int level ) throws JWaveException {
+    int rows = m.length, cols = rows == 0 ? 0 : m[ 0 ].length;
+    if( _taps == null ) {
+      double[ ][ ] out = new double[ rows ][ ];
+      for( int i = 0; i < rows; i++ )
+        out[ i ] = fwd ? super.forward( m[ i ], level ) : super.reverse( m[ i ], level );
+      return out;
+    }
+    double[ ] x = HipNative.pack( m ), y = new double[ x.length ];
+    HipNative.Taps t = _taps;
+    HipNative.check( HipNative.transformBatch( HipNative.ctx( ), 1, fwd, x, y, rows, cols, level,
+        t.L, t.tw, t.scale, t.lo, t.hi, t.loR, t.hiR ) );
+    return HipNative.unpack( y, rows, cols );
+  }
+}

@@ -10,6 +10,6 @@ from .transforms import (  # noqa: F401
     BasicTransform, Context, FastWaveletTransform, MODWTTransform, ParallelWaveletPacketTransform,
     PooledWaveletPacketTransform, Transform, WaveletPacketTransform, WaveletTransform,
     default_context, fwt_forward, fwt_reverse, modwt_filters, modwt_forward, modwt_inverse,
-    transform_2d, transform_3d, wpt_forward, wpt_reverse)
+    transform_2d, transform_3d, transform_axis, wpt_forward, wpt_reverse)
 
 __version__ = "0.1.0"

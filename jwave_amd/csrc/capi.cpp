@@ -926,6 +926,30 @@ static void check_2d(Kind k, bool fwd, int64_t rows, int64_t cols, int lvl_m, in
       body_2d(c, KIND, FWD, b, x, y, rows, cols, lvl_m, lvl_n);                                  \
     });                                                                                          \
   }
+// One axis of a contiguous [outer][len][inner] block: the per-dimension pass of
+// BasicTransform.java:369-395 (rows: inner = 1; columns: outer = 1).  The
+// sharded 2-D transform runs its column pass on a [rows][cols/W] slab with it.
+#define JWV_AXIS_DEV(NAME, KIND, FWD)                                                            \
+  int NAME(const double* x, double* y, int64_t outer, int64_t len, int64_t inner, int level,    \
+           const jwv_taps* t, jwv_ctx* c) {                                                      \
+    return guarded(c, [&] {                                                                      \
+      const Bank b = make_bank(t);                                                               \
+      if (outer < 0 || inner < 0) throw Fail{JWV_ERR_BAD_CALL, "negative dimension"};           \
+      check_1d(KIND, FWD, len, level);                                                           \
+      if (outer == 0 || len == 0 || inner == 0) return;                                          \
+      if (inner > (int64_t(1) << 30)) throw Fail{JWV_ERR_BAD_CALL, "inner dimension too large"}; \
+      need_device_ptrs(x, y);                                                                    \
+      const size_t tot = (size_t)(outer * len * inner);                                          \
+      check_overlap(x, tot, y, tot);                                                             \
+      const AxisView v = cview(len, inner);                                                      \
+      axis_fn(KIND, FWD)(c, b, Axis{x, v, y, v, outer, (int)len, (int)inner}, level);           \
+    });                                                                                          \
+  }
+JWV_AXIS_DEV(jwv_fwt_axis_fwd_f64_dev, Kind::FWT, true)
+JWV_AXIS_DEV(jwv_fwt_axis_rev_f64_dev, Kind::FWT, false)
+JWV_AXIS_DEV(jwv_wpt_axis_fwd_f64_dev, Kind::WPT, true)
+JWV_AXIS_DEV(jwv_wpt_axis_rev_f64_dev, Kind::WPT, false)
+
 JWV_2D(jwv_fwt2d_fwd_f64, Kind::FWT, true)
 JWV_2D(jwv_fwt2d_rev_f64, Kind::FWT, false)
 JWV_2D_DEV(jwv_fwt2d_fwd_f64_dev, Kind::FWT, true)

@@ -1,0 +1,199 @@
+"""Multi-GPU sharding of the hot path: one process per GPU, torch.distributed
+(backend "nccl" = RCCL over xGMI on MI355X; "gloo" for the CPU tests).
+
+What shards, and how:
+
+* Batches of signals (FWT/WPT batch, config 4): contiguous row blocks per rank,
+  no data-path collective (`shard_range`, `batch_forward/reverse`).
+* 2-D FWT (config 3, BasicTransform.java:361-474): row block per rank -> row
+  pass -> all-to-all transpose of [R/W x C/W] blocks -> column pass on the
+  [R][C/W] slab.  The forward result stays in that column-slab layout, which
+  is exactly what the sharded reverse consumes; `gather_cols` assembles it.
+* MODWT of one long signal (config 5, MODWTTransform.java:256-375): contiguous
+  slices; forward receives a left halo of H = (L-1)(2^J - 1) samples from its
+  ring predecessor, inverse a right halo of H columns of all J+1 rows from its
+  successor (one send/recv pair per direction).  Each rank then runs the
+  ordinary single-GPU transform on its extended slice as a periodic signal of
+  length n_local + H; the wrap only reaches the H outputs that are dropped, and
+  every kept output is summed from the same values in the same order, so the
+  sharded result is bit-identical to the single-GPU one.
+* One long 1-D FWT (config 2) does not shard: replicas only.
+
+Per-rank compute goes through a backend object; `HipBackend` (the only one in
+the package) calls the C ABI on the rank's GPU.  Tests substitute the CPU
+oracle to exercise the exchange logic with gloo on CPU.
+"""
+import torch
+import torch.distributed as dist
+
+from . import transforms as T
+
+
+def shard_range(total, world, rank):
+    """Contiguous block split: (start, count) of rank `rank`; the first
+    total % world ranks get one extra item."""
+    base, extra = divmod(int(total), int(world))
+    start = rank * base + min(rank, extra)
+    return start, base + (1 if rank < extra else 0)
+
+
+class HipBackend:
+    """Per-rank compute on this rank's GPU through libjwave_hip.so."""
+
+    def __init__(self, ctx=None):
+        self.ctx = ctx
+
+    def rows(self, x, w, level, forward, kind="fwt"):
+        f = T.fwt_forward if forward else T.fwt_reverse
+        return f(x, w, level, self.ctx, kind=kind)
+
+    def cols(self, x, w, level, forward, kind="fwt"):
+        # [R][cw] slab: transform along dim 0 (outer = 1, inner = cw)
+        return T.transform_axis(x, w, level, 0, forward, self.ctx, kind=kind)
+
+    def modwt_fwd(self, x, w, J):
+        return T.modwt_forward(x, w, J, self.ctx)
+
+    def modwt_inv(self, c, w):
+        return T.modwt_inverse(c, w, self.ctx)
+
+
+def _world(group):
+    return dist.get_world_size(group), dist.get_rank(group)
+
+
+# --------------------------------------------------------------- batches
+def batch_forward(x_local, w, level, backend, kind="fwt"):
+    """This rank's block of a sharded batch ([b_local][n]); no collective."""
+    return backend.rows(x_local, w, level, True, kind)
+
+
+def batch_reverse(y_local, w, level, backend, kind="fwt"):
+    return backend.rows(y_local, w, level, False, kind)
+
+
+def gather_rows(local, total, group=None):
+    """All-gather of contiguous row blocks (uneven blocks padded) -> [total][...]."""
+    W, _ = _world(group)
+    counts = [shard_range(total, W, r)[1] for r in range(W)]
+    mx = max(counts)
+    pad = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    pad[:local.shape[0]] = local
+    parts = [torch.empty_like(pad) for _ in range(W)]
+    dist.all_gather(parts, pad, group=group)
+    return torch.cat([p[:c] for p, c in zip(parts, counts)], 0)
+
+
+# --------------------------------------------------------------- 2-D FWT
+def _check_2d(rows, cols, W):
+    if rows % W or cols % W:
+        raise ValueError("sharded 2-D transform needs rows and cols divisible by the world size "
+                         "(%d x %d over %d ranks)" % (rows, cols, W))
+
+
+def _transpose_rows_to_cols(a, W, group):
+    """[rw][C] row block -> [R][cw] column slab (all-to-all of [rw][cw] blocks)."""
+    rw, C = a.shape
+    cw = C // W
+    send = a.reshape(rw, W, cw).permute(1, 0, 2).contiguous()  # [W][rw][cw], chunk j -> rank j
+    recv = torch.empty_like(send)                              # chunk i <- rank i's rows
+    dist.all_to_all_single(recv, send, group=group)
+    return recv.reshape(W * rw, cw)
+
+
+def _transpose_cols_to_rows(b, W, group):
+    """[R][cw] column slab -> [rw][C] row block (inverse of the above)."""
+    R, cw = b.shape
+    rw = R // W
+    send = b.reshape(W, rw, cw).contiguous()   # chunk i = rows of rank i
+    recv = torch.empty_like(send)              # chunk j = my rows of rank j's columns
+    dist.all_to_all_single(recv, send, group=group)
+    return recv.permute(1, 0, 2).reshape(rw, W * cw)
+
+
+def forward_2d(x_rows, rows, cols, w, lvl_m, lvl_n, backend, group=None, kind="fwt"):
+    """BasicTransform.forward(double[][], lvlM, lvlN) (BasicTransform.java:361-399)
+    sharded: x_rows = this rank's [rows/W][cols] block; returns this rank's
+    [rows][cols/W] column slab of the result."""
+    W, _ = _world(group)
+    _check_2d(rows, cols, W)
+    a = backend.rows(x_rows, w, lvl_n, True, kind)
+    b = _transpose_rows_to_cols(a, W, group)
+    return backend.cols(b, w, lvl_m, True, kind)
+
+
+def reverse_2d(y_cols, rows, cols, w, lvl_m, lvl_n, backend, group=None, kind="fwt"):
+    """BasicTransform.reverse(double[][], lvlM, lvlN) (BasicTransform.java:436-474)
+    sharded: y_cols = this rank's [rows][cols/W] slab; returns its
+    [rows/W][cols] row block of the reconstruction."""
+    W, _ = _world(group)
+    _check_2d(rows, cols, W)
+    b = backend.cols(y_cols, w, lvl_m, False, kind)
+    a = _transpose_cols_to_rows(b, W, group)
+    return backend.rows(a, w, lvl_n, False, kind)
+
+
+def gather_cols(slab, group=None):
+    """[R][cw] column slabs of all ranks -> the full [R][C] matrix."""
+    W, _ = _world(group)
+    parts = [torch.empty_like(slab) for _ in range(W)]
+    dist.all_gather(parts, slab.contiguous(), group=group)
+    return torch.cat(parts, 1)
+
+
+# --------------------------------------------------------------- MODWT
+def modwt_halo(L, J):
+    """Samples of context a level-J MODWT output needs on one side:
+    sum_j (L-1) 2^(j-1) (MODWTTransform.java:618-630 upsampled filter spans)."""
+    return (L - 1) * ((1 << J) - 1)
+
+
+def _ring_exchange(send, recv, to, frm, group):
+    reqs = [dist.isend(send.contiguous(), to, group=group),
+            dist.irecv(recv, frm, group=group)]
+    for r in reqs:
+        r.wait()
+
+
+def _check_modwt(n_global, J, counts, H):
+    # the reference's own checks (MODWTTransform.java:257-282) on the global N
+    T._check_modwt_levels(n_global, J)
+    if min(counts) < H:
+        raise ValueError("sharded MODWT needs every slice >= the halo (%d < %d)"
+                         % (min(counts), H))
+
+
+def modwt_forward(x_local, n_global, w, J, backend, group=None):
+    """forwardMODWT of one signal sharded in contiguous slices
+    (shard_range(n_global, W, rank)): returns this rank's [J+1][n_local] block
+    of [W_1 .. W_J, V_J]."""
+    W, rank = _world(group)
+    counts = [shard_range(n_global, W, r)[1] for r in range(W)]
+    H = modwt_halo(w.mother_wavelength, J)
+    _check_modwt(n_global, J, counts, H)
+    if W == 1:
+        return backend.modwt_fwd(x_local, w, J)
+    halo = torch.empty(H, dtype=x_local.dtype, device=x_local.device)
+    # my last H samples -> successor's left halo; predecessor's last H -> mine
+    _ring_exchange(x_local[-H:], halo, (rank + 1) % W, (rank - 1) % W, group)
+    ext = torch.cat([halo, x_local])
+    c = backend.modwt_fwd(ext, w, J)
+    return c[:, H:].contiguous()
+
+
+def modwt_inverse(c_local, n_global, w, backend, group=None):
+    """inverseMODWT of a sharded coefficient block [J+1][n_local]: returns this
+    rank's slice of the reconstruction."""
+    W, rank = _world(group)
+    J = c_local.shape[0] - 1
+    counts = [shard_range(n_global, W, r)[1] for r in range(W)]
+    H = modwt_halo(w.mother_wavelength, J)
+    _check_modwt(n_global, J, counts, H)
+    if W == 1:
+        return backend.modwt_inv(c_local, w)
+    halo = torch.empty((J + 1, H), dtype=c_local.dtype, device=c_local.device)
+    # my first H columns -> predecessor's right halo; successor's -> mine
+    _ring_exchange(c_local[:, :H], halo, (rank - 1) % W, (rank + 1) % W, group)
+    ext = torch.cat([c_local, halo], 1).contiguous()
+    x = backend.modwt_inv(ext, w)
+    return x[:c_local.shape[1]].contiguous()

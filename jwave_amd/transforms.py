@@ -232,6 +232,22 @@ def transform_3d(x, wavelet, lvl_p, lvl_q, lvl_r, forward=True, ctx=None, kind="
                 (p, q, r, int(lvl_p), int(lvl_q), int(lvl_r), _TapsHolder.of(wavelet)))
 
 
+def transform_axis(x, wavelet, level, axis_len_dim=1, forward=True, ctx=None, kind="fwt"):
+    """FWT/WPT of every line along one dimension of a contiguous device array
+    (the per-dimension pass of BasicTransform.java:369-395).  x: float64 CUDA
+    tensor; the transformed dimension is `axis_len_dim`, everything before it
+    is `outer`, everything after it is `inner`."""
+    if not (_is_torch(x) and x.is_cuda):
+        raise JWaveError("transform_axis takes a float64 device tensor")
+    shape = tuple(x.shape)
+    outer = int(np.prod(shape[:axis_len_dim], dtype=np.int64))
+    ln = int(shape[axis_len_dim])
+    inner = int(np.prod(shape[axis_len_dim + 1:], dtype=np.int64))
+    d = "fwd" if forward else "rev"
+    return _run(None, "jwv_%s_axis_%s_f64_dev" % (kind, d), ctx, x, shape,
+                (outer, ln, inner, int(level), _TapsHolder.of(wavelet)))
+
+
 def modwt_forward(x, wavelet, J, ctx=None):
     n = x.shape[0]
     return _run("jwv_modwt_fwd_f64", "jwv_modwt_fwd_f64_dev", ctx, x, (int(J) + 1, n),
@@ -438,6 +454,23 @@ class ParallelWaveletPacketTransform(WaveletPacketTransform):
     """ParallelWaveletPacketTransform.java: same math as the sequential WPT."""
 
 
+def _check_modwt_levels(n, J):
+    """MODWTTransform.forwardMODWT's checks, in the reference's order
+    (MODWTTransform.java:257-282); n = 0 skips the theoretical-limit check
+    (empty input returns J+1 empty rows)."""
+    if J < 1:
+        raise ValueError("MODWTTransform#forwardMODWT - decomposition level must be at least 1,"
+                         " requested: %d" % J)
+    if J > MAX_DECOMPOSITION_LEVEL:
+        raise ValueError("MODWTTransform#forwardMODWT - maximum supported decomposition level"
+                         " is %d, requested: %d" % (MAX_DECOMPOSITION_LEVEL, J))
+    if n > 0:
+        theo = int(n).bit_length() - 1
+        if J > theo:
+            raise ValueError("Decomposition level %d exceeds theoretical limit %d for signal length"
+                             " %d" % (J, theo, n))
+
+
 class MODWTTransform(WaveletTransform):
     """MODWTTransform.java:104-913 (DIRECT convolution semantics)."""
 
@@ -452,19 +485,10 @@ class MODWTTransform(WaveletTransform):
         return MAX_DECOMPOSITION_LEVEL
 
     def forwardMODWT(self, data, maxLevel):  # noqa: N802,N803 — :256-306
-        if maxLevel < 1:
-            raise ValueError("MODWTTransform#forwardMODWT - decomposition level must be at least 1,"
-                             " requested: %d" % maxLevel)
-        if maxLevel > MAX_DECOMPOSITION_LEVEL:
-            raise ValueError("MODWTTransform#forwardMODWT - maximum supported decomposition level"
-                             " is %d, requested: %d" % (MAX_DECOMPOSITION_LEVEL, maxLevel))
         if data is None or len(data) == 0:
+            _check_modwt_levels(0, maxLevel)
             return np.zeros((maxLevel + 1, 0))
-        n = len(data)
-        theo = n.bit_length() - 1
-        if maxLevel > theo:
-            raise ValueError("Decomposition level %d exceeds theoretical limit %d for signal length"
-                             " %d" % (maxLevel, theo, n))
+        _check_modwt_levels(len(data), maxLevel)
         return modwt_forward(data, self._wavelet, maxLevel, self._ctx)
 
     def inverseMODWT(self, coefficients):  # noqa: N802 — :337-375

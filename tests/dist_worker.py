@@ -1,0 +1,117 @@
+"""One rank of the multi-process tests of jwave_amd.distributed (gloo on CPU, or
+nccl on GPUs with --backend nccl).  Launched by tests/test_distributed.py as
+separate processes; exits 0 when every case matches the single-process result.
+
+On CPU the per-rank compute is the oracle (OracleBackend below — test
+infrastructure); on GPU it is jwave_amd.distributed.HipBackend, and the
+reference result is still the oracle on the full input.
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import oracle  # noqa: E402
+import jwave_amd as jw  # noqa: E402
+from jwave_amd import distributed as D  # noqa: E402
+
+
+class OracleBackend:
+    """Per-rank compute on the CPU oracle (tests only)."""
+
+    def rows(self, x, w, level, forward, kind="fwt"):
+        return torch.from_numpy(oracle.batch(kind, forward, w, x.numpy(), level))
+
+    def cols(self, x, w, level, forward, kind="fwt"):
+        y = oracle.batch(kind, forward, w, np.ascontiguousarray(x.numpy().T), level)
+        return torch.from_numpy(np.ascontiguousarray(y.T))
+
+    def modwt_fwd(self, x, w, J):
+        return torch.from_numpy(oracle.modwt_forward(w, x.numpy(), J))
+
+    def modwt_inv(self, c, w):
+        return torch.from_numpy(oracle.modwt_inverse(w, c.numpy()))
+
+
+def same(a, b, what):
+    a = a.detach().cpu().numpy() if torch.is_tensor(a) else a
+    if a.shape != b.shape or not np.array_equal(a, b):
+        d = np.abs(a - b).max() if a.shape == b.shape else "shape %s vs %s" % (a.shape, b.shape)
+        raise AssertionError("%s: mismatch (%s)" % (what, d))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rank", type=int, required=True)
+    ap.add_argument("--world", type=int, required=True)
+    ap.add_argument("--port", type=int, required=True)
+    ap.add_argument("--backend", default="gloo")
+    a = ap.parse_args()
+    if a.backend == "nccl":
+        torch.cuda.set_device(a.rank)
+        dev = torch.device("cuda", a.rank)
+        be = D.HipBackend(jw.Context(a.rank))
+    else:
+        dev = torch.device("cpu")
+        be = OracleBackend()
+    dist.init_process_group(a.backend, init_method="tcp://127.0.0.1:%d" % a.port,
+                            rank=a.rank, world_size=a.world)
+    W, r = a.world, a.rank
+
+    def put(arr):
+        return torch.from_numpy(np.ascontiguousarray(arr)).to(dev)
+
+    # ---- batches (config 4 shape, small): contiguous row blocks, no collective
+    for kind, wname, total, n, lev in (("wpt", "Symlet8", 7, 256, 3), ("fwt", "Daubechies4", 5, 64, 6)):
+        w = jw.by_class(wname)
+        full = oracle.java_random_doubles(42, total * n).reshape(total, n)
+        s, c = D.shard_range(total, W, r)
+        y = D.batch_forward(put(full[s:s + c]), w, lev, be, kind)
+        yg = D.gather_rows(y.cpu() if a.backend == "gloo" else y, total)
+        same(yg, oracle.batch(kind, True, w, full, lev), "%s batch fwd" % kind)
+        xr = D.batch_reverse(y, w, lev, be, kind)
+        same(D.gather_rows(xr, total), oracle.batch(kind, False, w,
+                                                    oracle.batch(kind, True, w, full, lev), lev),
+             "%s batch rev" % kind)
+
+    # ---- 2-D: row pass, all-to-all transpose, column pass
+    for wname, rows, cols, lm, ln in (("Daubechies8", 64, 128, 6, 7), ("Haar1", 32, 16, 2, 3),
+                                      ("Daubechies4", 128, 64, 5, 0)):
+        if rows % W or cols % W:
+            continue
+        w = jw.by_class(wname)
+        full = oracle.java_random_doubles(123456789, rows * cols).reshape(rows, cols)
+        rw = rows // W
+        yc = D.forward_2d(put(full[r * rw:(r + 1) * rw]), rows, cols, w, lm, ln, be)
+        ref = oracle.transform_2d("fwt", True, w, full, lm, ln)
+        same(D.gather_cols(yc), ref, "2d fwd %s" % wname)
+        xr = D.reverse_2d(yc, rows, cols, w, lm, ln, be)
+        same(D.gather_rows(xr, rows), oracle.transform_2d("fwt", False, w, ref, lm, ln),
+             "2d rev %s" % wname)
+
+    # ---- MODWT of one long signal: ring halo exchange
+    for wname, n, J in (("Daubechies4", 1000, 5), ("Haar1", 1001, 3), ("Daubechies8", 4096, 4)):
+        w = jw.by_class(wname)
+        full = oracle.java_random_doubles(42, n)
+        s, c = D.shard_range(n, W, r)
+        cf = D.modwt_forward(put(full[s:s + c]), n, w, J, be)
+        ref = oracle.modwt_forward(w, full, J)
+        got = D.gather_rows(cf.t().contiguous(), n).t()
+        same(got, ref, "modwt fwd %s n=%d" % (wname, n))
+        xr = D.modwt_inverse(cf, n, w, be)
+        same(D.gather_rows(xr, n), oracle.modwt_inverse(w, ref), "modwt inv %s n=%d" % (wname, n))
+
+    dist.barrier()
+    dist.destroy_process_group()
+    print("rank %d OK" % r, flush=True)
+
+
+if __name__ == "__main__":
+    main()

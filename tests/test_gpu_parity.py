@@ -315,3 +315,26 @@ def test_facade_and_classes(ctx):
         for lev in (0, 1, 2):
             np.testing.assert_allclose(t.reverse(t.forward(x, lev), lev), x, atol=1e-8)
     assert jw.Transform(jw.FastWaveletTransform(jw.by_class("Haar1"), ctx)).forward(np.ones(3)) is None
+
+
+@pytest.mark.parametrize("kind,wname,R,cw,lev", [
+    ("fwt", "Daubechies4", 1024, 24, 10), ("fwt", "Symlet8", 16384, 8, 14),
+    ("fwt", "Haar1", 64, 3, 6), ("fwt", "Daubechies8", 32768, 16, 7),
+    ("wpt", "Symlet8", 4096, 8, 6), ("wpt", "Daubechies4", 256, 5, 8)])
+def test_axis_columns(ctx, kind, wname, R, cw, lev):
+    """jwv_{fwt,wpt}_axis_*_dev on a [R][cw] column slab (the sharded 2-D
+    column pass) vs the oracle on the transposed lines, both directions."""
+    import torch
+    w = jw.by_class(wname)
+    x = rnd(R * cw, seed=7).reshape(R, cw)
+    ref = oracle.batch(kind, True, w, np.ascontiguousarray(x.T), lev).T
+    xd = torch.from_numpy(x).cuda()
+    y = T.transform_axis(xd, w, lev, 0, True, ctx, kind=kind)
+    assert_exact(y.cpu().numpy(), ref, "%s axis fwd" % kind)
+    back = oracle.batch(kind, False, w, np.ascontiguousarray(ref.T), lev).T
+    xr = T.transform_axis(y, w, lev, 0, False, ctx, kind=kind)
+    assert_exact(xr.cpu().numpy(), back, "%s axis rev" % kind)
+    # rows of a 3-D block: middle axis of [2][R][cw]
+    x3 = torch.stack([xd, xd.flip(0)])
+    y3 = T.transform_axis(x3, w, lev, 1, True, ctx, kind=kind)
+    assert_exact(y3[0].cpu().numpy(), ref, "%s axis fwd 3d" % kind)
