@@ -659,6 +659,26 @@ int Geo::stream_blocks_per_cu() {
   static const int n = env_int("JWV_STREAM_BPC", 2);
   return n < 1 ? 1 : (n > 8 ? 8 : n);
 }
+bool Geo::fwt1() {
+  static const bool p = env_int("JWV_FWT1", 1) != 0;
+  return p;
+}
+int Geo::fwd1_t() {
+  static const int n = env_int("JWV_FWD1_T", 4096) == 2048 ? 2048 : 4096;
+  return n;
+}
+int Geo::fwd1_nt() {
+  static const int n = env_int("JWV_FWD1_NT", 256) == 512 ? 512 : 256;
+  return n;
+}
+int Geo::rev1_t() {
+  static const int n = env_int("JWV_REV1_T", 2048) == 4096 ? 4096 : 2048;
+  return n;
+}
+int Geo::rev1_nt() {
+  static const int n = env_int("JWV_REV1_NT", 256) == 128 ? 128 : 256;
+  return n;
+}
 int Geo::stream_ntc() {
   static const int n = env_int("JWV_STREAM_NTC", 512) == 256 ? 256 : 512;
   return n;
@@ -676,9 +696,15 @@ hipError_t launch_fwt_rev_res(const Bank& b, bool fma, int C, const ResArgs& a, 
   JWV_MODE2(fwt_rev_res, b, C, a, s);
 }
 hipError_t launch_fwt_fwd_tile(const Bank& b, bool fma, int C, const TileArgs& a, hipStream_t s) {
+  hipError_t e = hipSuccess;
+  if (C == 1 && (fma ? fused::fwt_fwd_tile1(b, a, s, e) : exact::fwt_fwd_tile1(b, a, s, e)))
+    return e;
   JWV_MODE2(fwt_fwd_tile, b, C, a, s);
 }
 hipError_t launch_fwt_rev_tile(const Bank& b, bool fma, int C, const TileArgs& a, hipStream_t s) {
+  hipError_t e = hipSuccess;
+  if (C == 1 && (fma ? fused::fwt_rev_tile1(b, a, s, e) : exact::fwt_rev_tile1(b, a, s, e)))
+    return e;
   JWV_MODE2(fwt_rev_tile, b, C, a, s);
 }
 hipError_t launch_wpt_fwd_res(const Bank& b, bool fma, int C, const ResArgs& a, hipStream_t s) {

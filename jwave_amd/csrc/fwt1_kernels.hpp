@@ -1,0 +1,199 @@
+// fwt1_kernels.hpp — FWT tile kernels for contiguous signals (C = 1,
+// sample stride 1, every base pointer 16-B aligned) with compile-time
+// geometry: tap count L, tile T and fused level count K are template
+// arguments, so every level's window size, slot count and store guard is a
+// constant and the level loop unrolls into straight-line code.
+//
+// Same math and summation order as fwt_fwd_tile / fwt_rev_tile
+// (Wavelet.java:236-303; see fwt_kernels.hpp), so EXACT results stay
+// bit-identical.  Differences are structural only:
+//  * levels ping-pong between two LDS buffers: one barrier per level and no
+//    per-slot result registers held across a barrier;
+//  * detail / output stores use an SGPR base + 32-bit lane offset; the final
+//    synthesis level stores (x[2m], x[2m+1]) as one 16-B store;
+//  * reverse: the array-head pairs (Wavelet.java:284-296 wrap order) exist
+//    only in tile 0, so every other tile runs the branch-free interior form.
+#pragma once
+#include "fwt_kernels.hpp"
+
+namespace jwv {
+
+// ---------------------------------------------------------------- forward
+// Window after l fused levels: T/2^l own samples + (L-2)(2^(K-l) - 1) halo.
+template <int L, int T, int K>
+struct Fwd1Geo {
+  static constexpr int m(int l) { return (T >> l) + (L - 2) * ((1 << (K - l)) - 1); }
+  static constexpr int buf0() { return (m(0) + 2) & ~1; }  // + DMA overrun, even
+  static constexpr int lds_doubles() { return buf0() + ((m(1) + 1) & ~1); }
+};
+
+template <int L, int NT, int T, int K, bool FMA, int l>
+struct Fwd1Level {
+  // in: level-(l-1) window (m(l-1) samples); out: level-l approximation window.
+  // yd: this tile's first detail of level l; ya: first level-K approximation.
+  __device__ __forceinline__ static void run(const FwdTaps<L>& tp, const double* in, double* out,
+                                             double* __restrict__ yd0, int hl, int t,
+                                             double* __restrict__ ya) {
+    using G = Fwd1Geo<L, T, K>;
+    constexpr int mo = G::m(l);
+    constexpr int own = T >> l;
+    constexpr int R = (mo + NT - 1) / NT;
+    const int tid = threadIdx.x;
+    double* __restrict__ yd = yd0 + (hl >> 1) + (int64_t)t * own;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int p = tid + r * NT;
+      if ((r + 1) * NT <= mo || p < mo) {
+        double a, d;
+        fwd_pair<L, FMA>(tp, [&](int j) { return in[2 * p + j]; }, a, d);
+        if constexpr (l == K) {
+          ya[(int64_t)t * own + p] = a;  // mo == own at the last level
+        } else {
+          out[p] = a;
+        }
+        if (r * NT < own && ((r + 1) * NT <= own || p < own)) yd[p] = d;
+      }
+    }
+    if constexpr (l < K) {
+      __syncthreads();
+      Fwd1Level<L, NT, T, K, FMA, l + 1>::run(tp, out, const_cast<double*>(in), yd0, hl >> 1, t, ya);
+    }
+  }
+};
+
+// Grid: nouter * (h / T) blocks, tile-fastest, XCD-remapped like fwt_fwd_tile.
+// src: level input (length h, stride 1); dst: coefficient array of the
+// signal (details of level size hl at dst[hl/2 ..]); adst: level-K output.
+template <int L, int NT, int T, int K, bool FMA>
+__global__ __launch_bounds__(NT) void fwt_fwd_tile1(const double* __restrict__ src,
+                                                    int64_t s_src, double* __restrict__ dst,
+                                                    int64_t s_dst, double* __restrict__ adst,
+                                                    int64_t s_adst, int h, FwdTaps<L> tp) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  using G = Fwd1Geo<L, T, K>;
+  constexpr int M0 = G::m(0);
+  const int ntile = h / T;
+  const int nblk = gridDim.x;
+  int b = blockIdx.x;
+  if ((nblk & 7) == 0) b = (b & 7) * (nblk >> 3) + (b >> 3);
+  const int t = b % ntile;
+  const int64_t o = b / ntile;
+  const double* s = src + o * s_src;
+  const int msk = h - 1, base = t * T;
+  load_window<1, NT, (M0 + NT - 1) / NT>(lds, s, M0, true, 0, 1,
+                                          [&](int e) { return (int64_t)((base + e) & msk); });
+  dma_fence_barrier();
+  Fwd1Level<L, NT, T, K, FMA, 1>::run(tp, lds, lds + G::buf0(), dst + o * s_dst, h, t,
+                                      adst + o * s_adst);
+}
+
+// ---------------------------------------------------------------- reverse
+// Window of the level-l array (l = 0: the output): [tT/2^l - c_l, (t+1)T/2^l),
+// c_0 = 0, c_{l+1} = ceil_even(c_l/2 + Q-1) (fwt_rev_tile's B_{l+1} recursion
+// with every tile boundary even).  Needs T/2^K even.
+template <int L, int T, int K>
+struct Rev1Geo {
+  static constexpr int Q = L / 2;
+  static constexpr int c(int l) {
+    int cc = 0;
+    for (int k = 0; k < l; ++k) cc = ((cc / 2 + (Q - 1)) + 1) & ~1;
+    return cc;
+  }
+  static constexpr int len(int l) { return (T >> l) + c(l); }
+  // LDS: detail windows of levels K-1 .. 0 (each len(l+1)), then two
+  // approximation buffers: buf[1] (len(1)), buf[0] (len(2)).  Level l reads
+  // buf[(l+1)&1] and writes buf[l&1]; the initial level-K window goes to buf[K&1].
+  static constexpr int doff(int l) {  // offset of level l's detail window
+    int o = 0;
+    for (int k = K - 1; k > l; --k) o += len(k + 1);
+    return o;
+  }
+  static constexpr int dtotal() { return doff(-1); }
+  static constexpr int buf1() { return dtotal(); }
+  static constexpr int buf0() { return dtotal() + len(1); }
+  static constexpr int lds_doubles() {
+    return dtotal() + len(1) + (K >= 2 ? (len(2) > len(K) ? len(2) : len(K)) : 0);
+  }
+  static_assert(((T >> K) & 1) == 0, "T/2^K must be even");
+};
+
+template <int L, int NT, int T, int K, bool FMA, int l>
+struct Rev1Level {
+  __device__ __forceinline__ static void run(const RevTaps<L>& tp, double* lds, int t,
+                                             double* __restrict__ y) {
+    using G = Rev1Geo<L, T, K>;
+    constexpr int Q = G::Q;
+    constexpr int np = G::len(l) / 2;                    // pairs of this level's window
+    constexpr int off = G::c(l + 1) - G::c(l) / 2;       // local index of a[pair 0]
+    constexpr int R = (np + NT - 1) / NT;
+    const double* ab = lds + ((((l + 1) & 1) != 0) ? G::buf1() : G::buf0());
+    const double* db = lds + G::doff(l);
+    double* ob = lds + (((l & 1) != 0) ? G::buf1() : G::buf0());
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int ml = tid + r * NT;
+      if ((r + 1) * NT <= np || ml < np) {
+        const int li = off + ml;
+        double xe, xo;
+        rev_pair<L, FMA>(tp, ab + li, db + li, 1, xe, xo);
+        if (r == 0 && t == 0) {
+          // array head: global pair m = ml - c_l/2 in [0, Q-1) (tile 0 only)
+          const int mg = ml - G::c(l) / 2;
+          if (mg >= 0 && mg < Q - 1)
+            rev_pair_head<L, FMA>(
+                tp, mg, [=](int q) { return ab[li - q]; }, [=](int q) { return db[li - q]; }, xe,
+                xo);
+        }
+        if constexpr (l == 0) {
+          *reinterpret_cast<double2*>(y + (int64_t)t * T + 2 * ml) = make_double2(xe, xo);
+        } else {
+          *reinterpret_cast<double2*>(ob + 2 * ml) = make_double2(xe, xo);
+        }
+      }
+    }
+    if constexpr (l > 0) {
+      __syncthreads();
+      Rev1Level<L, NT, T, K, FMA, l - 1>::run(tp, lds, t, y);
+    }
+  }
+};
+
+// Grid: nouter * (hK / T) blocks.  asrc: level-K approximation (length
+// h1/2 = hK >> K); coef: the coefficient array (details of level size h at
+// coef[h/2 ..)); dst: output of length hK.
+template <int L, int NT, int T, int K, bool FMA>
+__global__ __launch_bounds__(NT) void fwt_rev_tile1(const double* __restrict__ asrc,
+                                                    int64_t s_a, const double* __restrict__ coef,
+                                                    int64_t s_c, double* __restrict__ dst,
+                                                    int64_t s_d, int hK, RevTaps<L> tp) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  using G = Rev1Geo<L, T, K>;
+  constexpr int MAXU = (G::len(1) + NT - 1) / NT;
+  const int ntile = hK / T;
+  const int nblk = gridDim.x;
+  int b = blockIdx.x;
+  if ((nblk & 7) == 0) b = (b & 7) * (nblk >> 3) + (b >> 3);
+  const int t = b % ntile;
+  const int64_t o = b / ntile;
+  const double* sa = asrc + o * s_a;
+  const double* sc = coef + o * s_c;
+  // every window in one burst: level-K approximation, then the details
+  {
+    const int BK = (t * T >> K) - G::c(K);
+    const int am = (hK >> K) - 1;
+    load_window<1, NT, MAXU>(lds + ((K & 1) ? G::buf1() : G::buf0()), sa, G::len(K), true, 0, 1,
+                             [&](int e) { return (int64_t)((BK + e) & am); });
+  }
+#pragma unroll
+  for (int l = K - 1; l >= 0; --l) {
+    const int half = hK >> (l + 1), hm = half - 1;
+    const int B = (t * T >> (l + 1)) - G::c(l + 1);
+    load_window<1, NT, MAXU>(lds + G::doff(l), sc, G::len(l + 1), true, 0, 1,
+                             [&](int e) { return (int64_t)half + ((B + e) & hm); });
+  }
+  dma_fence_barrier();
+  Rev1Level<L, NT, T, K, FMA, K - 1>::run(tp, lds, t, dst + o * s_d);
+}
+
+}  // namespace jwv
