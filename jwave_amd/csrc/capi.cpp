@@ -225,16 +225,38 @@ int rev_first(int len, int tw, int level) {
 }
 
 // ------------------------------------------------------------------ FWT axis
+// True when the C = 1 compile-time-geometry kernels (launch_fwt1.hip) take
+// every tiled pass of this axis transform: contiguous 16-B aligned rows, a
+// compiled-in tap count, an unscaled synthesis bank.  The planner then uses
+// their deeper passes (up to Geo::kFwt1KMax levels) and short tails.
+bool fast1(const Bank& b, const Axis& a, bool rev) {
+  if (!Geo::fwt1() || a.inner != 1 || jwv::static_l(b.L) == 0) return false;
+  if (rev && b.scale != 1.0) return false;
+  if (a.sv.pk != 1 || a.dv.pk != 1 || a.sv.s_len != 1 || a.dv.s_len != 1) return false;
+  if (!dma_view(a.src, a.sv, 1, 1)) return false;
+  if (rev && (((uintptr_t)a.dst & 15) || (a.outer > 1 && (a.dv.s_outer & 1)))) return false;
+  return true;
+}
+
 void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
   const int nlev = fwd_levels(a.len, b.tw, level);
   if (nlev == 0) return copy_axis(c, a);
   const int C = col_slab(a.inner), cap = Geo::res_cap(C), KM = Geo::fwt_k(C);
+  const bool f1 = fast1(b, a, false);
+  // levels of the tiled pass at level-input size h: KM, except that on the
+  // fwt1 path the pass that ends the tiled part runs on down to kFwt1FwdTail
+  auto pick_k = [&](int h, int rem) {
+    int K = std::min(rem, KM);
+    if (f1 && (h >> K) <= cap)
+      K = std::min(rem, std::min(exponent(h) - exponent(Geo::kFwt1FwdTail), Geo::kFwt1KMax));
+    return K;
+  };
   // workspace: the largest intermediate approximation
   {
     int h = a.len, rem = nlev;
     size_t need = 0;
     while (rem > 0 && h > cap) {
-      const int K = std::min(rem, KM);
+      const int K = pick_k(h, rem);
       if (K < rem) need = std::max(need, (size_t)a.outer * (size_t)(h >> K) * a.inner);
       h >>= K;
       rem -= K;
@@ -245,7 +267,7 @@ void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
   AxisView cv = a.sv;
   int h = a.len, rem = nlev, pp = 0;
   while (rem > 0 && h > cap) {
-    const int K = std::min(rem, KM);
+    const int K = pick_k(h, rem);
     const bool last = K == rem;
     double* ad = last ? a.dst : c->ws[pp].p;
     const AxisView av = last ? a.dv : cview(h >> K, a.inner);
@@ -269,7 +291,12 @@ void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
 void fwt_rev_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
   const int h = rev_first(a.len, b.tw, level);
   if (h == 0) return copy_axis(c, a);
-  const int C = col_slab(a.inner), cap = Geo::res_cap(C), KM = Geo::fwt_k(C);
+  const int C = col_slab(a.inner);
+  // fwt1 path, signal longer than one resident block: the resident tail stops
+  // at kFwt1RevTail and the tiled passes take up to kFwt1KMax levels
+  const bool f1 = fast1(b, a, true) && a.len > Geo::res_cap(C);
+  const int cap = f1 ? Geo::kFwt1RevTail : Geo::res_cap(C);
+  const int KM = f1 ? Geo::kFwt1KMax : Geo::fwt_k(C);
   // workspace sizing
   {
     size_t need = 0;
@@ -663,22 +690,6 @@ bool Geo::fwt1() {
   static const bool p = env_int("JWV_FWT1", 1) != 0;
   return p;
 }
-int Geo::fwd1_t() {
-  static const int n = env_int("JWV_FWD1_T", 4096) == 2048 ? 2048 : 4096;
-  return n;
-}
-int Geo::fwd1_nt() {
-  static const int n = env_int("JWV_FWD1_NT", 256) == 512 ? 512 : 256;
-  return n;
-}
-int Geo::rev1_t() {
-  static const int n = env_int("JWV_REV1_T", 2048) == 4096 ? 4096 : 2048;
-  return n;
-}
-int Geo::rev1_nt() {
-  static const int n = env_int("JWV_REV1_NT", 256) == 128 ? 128 : 256;
-  return n;
-}
 int Geo::stream_ntc() {
   static const int n = env_int("JWV_STREAM_NTC", 512) == 256 ? 256 : 512;
   return n;
@@ -690,21 +701,30 @@ bool Geo::rev_pref() {
 #define JWV_MODE2(name, ...) \
   return fma ? fused::name(__VA_ARGS__) : exact::name(__VA_ARGS__)
 hipError_t launch_fwt_fwd_res(const Bank& b, bool fma, int C, const ResArgs& a, hipStream_t s) {
+  hipError_t e = hipSuccess;
+  if (C == 1 && (fma ? fused::fwt_fwd_res1(b, a, s, e) : exact::fwt_fwd_res1(b, a, s, e)))
+    return e;
   JWV_MODE2(fwt_fwd_res, b, C, a, s);
 }
 hipError_t launch_fwt_rev_res(const Bank& b, bool fma, int C, const ResArgs& a, hipStream_t s) {
+  hipError_t e = hipSuccess;
+  if (C == 1 && (fma ? fused::fwt_rev_res1(b, a, s, e) : exact::fwt_rev_res1(b, a, s, e)))
+    return e;
   JWV_MODE2(fwt_rev_res, b, C, a, s);
 }
 hipError_t launch_fwt_fwd_tile(const Bank& b, bool fma, int C, const TileArgs& a, hipStream_t s) {
   hipError_t e = hipSuccess;
   if (C == 1 && (fma ? fused::fwt_fwd_tile1(b, a, s, e) : exact::fwt_fwd_tile1(b, a, s, e)))
     return e;
+  // the generic kernels are compiled for at most fwt_k(C) fused levels
+  if (a.K > Geo::fwt_k(C)) return hipErrorInvalidValue;
   JWV_MODE2(fwt_fwd_tile, b, C, a, s);
 }
 hipError_t launch_fwt_rev_tile(const Bank& b, bool fma, int C, const TileArgs& a, hipStream_t s) {
   hipError_t e = hipSuccess;
   if (C == 1 && (fma ? fused::fwt_rev_tile1(b, a, s, e) : exact::fwt_rev_tile1(b, a, s, e)))
     return e;
+  if (a.K > Geo::fwt_k(C)) return hipErrorInvalidValue;
   JWV_MODE2(fwt_rev_tile, b, C, a, s);
 }
 hipError_t launch_wpt_fwd_res(const Bank& b, bool fma, int C, const ResArgs& a, hipStream_t s) {

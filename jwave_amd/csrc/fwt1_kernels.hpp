@@ -12,7 +12,7 @@
 //  * detail / output stores use an SGPR base + 32-bit lane offset; the final
 //    synthesis level stores (x[2m], x[2m+1]) as one 16-B store;
 //  * reverse: the array-head pairs (Wavelet.java:284-296 wrap order) exist
-//    only in tile 0, so every other tile runs the branch-free interior form.
+//    only in the first tiles' windows; every other block skips the head test.
 #pragma once
 #include "fwt_kernels.hpp"
 
@@ -55,7 +55,7 @@ struct Fwd1Level {
       }
     }
     if constexpr (l < K) {
-      __syncthreads();
+      lds_barrier();
       Fwd1Level<L, NT, T, K, FMA, l + 1>::run(tp, out, const_cast<double*>(in), yd0, hl >> 1, t, ya);
     }
   }
@@ -137,9 +137,12 @@ struct Rev1Level {
         const int li = off + ml;
         double xe, xo;
         rev_pair<L, FMA>(tp, ab + li, db + li, 1, xe, xo);
-        if (r == 0 && t == 0) {
-          // array head: global pair m = ml - c_l/2 in [0, Q-1) (tile 0 only)
-          const int mg = ml - G::c(l) / 2;
+        // array-head pairs (global pair index in [0, Q-1)): in tile 0, and in
+        // the halo of the next tiles at deep levels where c_l > T/2^l.  The
+        // window's first global pair pbase decides for the whole block.
+        const int pbase = t * (T >> (l + 1)) - G::c(l) / 2;
+        if (r == 0 && pbase < Q - 1) {
+          const int mg = pbase + ml;
           if (mg >= 0 && mg < Q - 1)
             rev_pair_head<L, FMA>(
                 tp, mg, [=](int q) { return ab[li - q]; }, [=](int q) { return db[li - q]; }, xe,
@@ -153,7 +156,7 @@ struct Rev1Level {
       }
     }
     if constexpr (l > 0) {
-      __syncthreads();
+      lds_barrier();
       Rev1Level<L, NT, T, K, FMA, l - 1>::run(tp, lds, t, y);
     }
   }

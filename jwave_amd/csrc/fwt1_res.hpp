@@ -1,0 +1,250 @@
+// fwt1_res.hpp — resident FWT kernels for contiguous signals (C = 1, stride
+// 1, 16-B aligned rows) with a compiled-in tap count.  One block holds a
+// whole level input (<= CAP samples) in LDS and runs the remaining levels:
+// the deep tail of a long 1-D signal (one block, latency-bound) and batches of
+// rows (one block per row).
+//
+// Latency rules for the tail, where one wave often works alone:
+//  * every level issues all of its LDS reads before its first FP64 op (one
+//    LDS round trip per level, not one per tap);
+//  * the reverse array-head pairs (Wavelet.java:284-296 order) sum from
+//    registers: no LDS access inside a divergent branch;
+//  * barriers are LDS-only (lds_barrier), so the detail stores of the forward
+//    levels stay in flight across them.
+// Math and summation order are those of fwt_fwd_res / fwt_rev_res.
+#pragma once
+#include "fwt_kernels.hpp"
+
+namespace jwv {
+
+// a, d of pair p of a level of size h (mask msk = h-1) from LDS, wrap by mask.
+template <int L, bool FMA>
+__device__ __forceinline__ void fwd_pair_wrap(const FwdTaps<L>& tp, const double* in, int p,
+                                              int msk, double& a, double& d) {
+  double x[L];
+#pragma unroll
+  for (int j = 0; j < L; ++j) x[j] = in[(2 * p + j) & msk];
+  fwd_pair<L, FMA>(tp, [&](int j) { return x[j]; }, a, d);
+}
+
+// Synthesis pair m of a level of size h >= L: a = lds[0, half), d =
+// lds[half, h).  Interior pairs (m >= Q-1) sum q descending; head pairs use
+// rev_pair_head's order on the same register values.
+template <int L, bool FMA>
+__device__ __forceinline__ void rev_pair_wrap(const RevTaps<L>& tp, const double* lds, int half,
+                                              int m, double& xe, double& xo) {
+  constexpr int Q = (L + 1) / 2;
+  const int hm = half - 1;
+  double av[Q], dv[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int i = (m - q) & hm;
+    av[q] = lds[i];
+    dv[q] = lds[half + i];
+  }
+  // rev_pair reads A[-q*st]: hand it the register arrays through a view with
+  // st = -1 on a pointer to element 0 (A[-q*(-1)] = av[q]).
+  rev_pair<L, FMA>(tp, av, dv, -1, xe, xo);
+  if (m < Q - 1)
+    rev_pair_head<L, FMA>(tp, m, [&](int q) { return av[q]; }, [&](int q) { return dv[q]; }, xe,
+                          xo);
+}
+
+// Levels with h < L wrap several times: Wavelet.reverse's scatter order
+// (i ascending, j ascending) for output k, from registers.
+template <int L, bool FMA>
+__device__ __forceinline__ double rev_small_regs(const RevTaps<L>& tp, const double* av,
+                                                 const double* dv, int h, int k) {
+  constexpr int HM = L / 2;  // h < L  =>  half < L/2
+  const int half = h >> 1;
+  double x = 0.0;
+#pragma unroll
+  for (int i = 0; i < HM; ++i)
+#pragma unroll
+    for (int j = 0; j < L; ++j)
+      if (i < half && ((2 * i + j) & (h - 1)) == k) {
+        double t = av[i] * tp.lo_r[j];
+        t = mac<FMA>(t, dv[i], tp.hi_r[j]);
+        x += t;
+      }
+  return x;
+}
+
+// ====================================================================
+// Forward, resident, C = 1.  src row: level input of length h0 (DMA-able);
+// dst row: coefficient array (details of level size h at dst[h/2, h), final
+// approximation at dst[0, h_end)).
+// ====================================================================
+template <int L, int NT, int CAP, bool FMA>
+__global__ __launch_bounds__(NT) void fwt_fwd_res1(const double* __restrict__ src, int64_t s_src,
+                                                   double* __restrict__ dst, int64_t s_dst, int h0,
+                                                   int nlev, FwdTaps<L> tp) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  constexpr int RM = CAP / 2 / NT > 0 ? CAP / 2 / NT : 1;
+  const int64_t o = blockIdx.x;
+  double* __restrict__ y = dst + o * s_dst;
+  const int tid = threadIdx.x;
+  JWV_STAMP(0);
+  load_window<1, NT, (CAP + NT - 1) / NT>(lds, src + o * s_src, h0, true, 0, 1,
+                                          [&](int e) { return (int64_t)e; });
+  dma_fence_barrier();
+  JWV_STAMP(1);
+
+  int h = h0, lev = 0;
+  // block-wide levels: np = h/2 > 64 pairs, a power of two
+  for (; lev < nlev && (h >> 1) > 64; ++lev, h >>= 1) {
+    JWV_STAMP(2 + lev);
+    const int half = h >> 1, msk = h - 1;
+    double av[RM];
+    auto slot = [&](int r) {
+      const int p = tid + r * NT;
+      double a, d;
+      fwd_pair_wrap<L, FMA>(tp, lds, p, msk, a, d);
+      av[r] = a;
+      y[half + p] = d;
+    };
+    const int R = half / NT;  // 0 when half < NT
+    if (R <= 1) {
+      if (tid < half) slot(0);
+    } else if (R == 2) {
+#pragma unroll
+      for (int r = 0; r < 2; ++r) slot(r);
+    } else if (R == 4) {
+#pragma unroll
+      for (int r = 0; r < (RM < 4 ? RM : 4); ++r) slot(r);
+    } else if (R == 8) {
+#pragma unroll
+      for (int r = 0; r < (RM < 8 ? RM : 8); ++r) slot(r);
+    } else {
+#pragma unroll
+      for (int r = 0; r < (RM < 16 ? RM : 16); ++r) slot(r);
+    }
+    lds_barrier();
+    if (R <= 1) {
+      if (tid < half) lds[tid] = av[0];
+    } else {
+#pragma unroll
+      for (int r = 0; r < RM; ++r)
+        if (r < R) lds[tid + r * NT] = av[r];
+    }
+    lds_barrier();
+  }
+  // small levels: wave 0 alone (no block barriers)
+  if (lev < nlev) {
+    if (tid < 64) {
+      int hh = h;
+      for (int lv = lev; lv < nlev; ++lv, hh >>= 1) {
+        JWV_STAMP(2 + lv);
+        const int half = hh >> 1;
+        const bool v = tid < half;
+        const int p = v ? tid : half - 1;
+        double a, d;
+        fwd_pair_wrap<L, FMA>(tp, lds, p, hh - 1, a, d);
+        if (v) y[half + p] = d;
+        wave_lds_sync();
+        if (v) lds[p] = a;
+        wave_lds_sync();
+      }
+    }
+    h >>= (nlev - lev);
+    lds_barrier();
+  }
+  JWV_STAMP(40);
+  for (int q = tid; q < h; q += NT) y[q] = lds[q];
+  JWV_STAMP(42);
+}
+
+// ====================================================================
+// Reverse, resident, C = 1.  src row: coefficient prefix [0, htop) with
+// htop = h0 << (nlev-1) (h0 = first synthesis level size); dst row: [0, htop).
+// ====================================================================
+template <int L, int NT, int CAP, bool FMA>
+__global__ __launch_bounds__(NT) void fwt_rev_res1(const double* __restrict__ src, int64_t s_src,
+                                                   double* __restrict__ dst, int64_t s_dst, int h0,
+                                                   int nlev, RevTaps<L> tp) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  constexpr int RM = CAP / 2 / NT > 0 ? CAP / 2 / NT : 1;
+  const int64_t o = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int htop = nlev > 0 ? (h0 << (nlev - 1)) : h0;
+  JWV_STAMP(0);
+  load_window<1, NT, (CAP + NT - 1) / NT>(lds, src + o * s_src, htop, true, 0, 1,
+                                          [&](int e) { return (int64_t)e; });
+  dma_fence_barrier();
+  JWV_STAMP(1);
+
+  int h = h0, lev = 0;
+  if (nlev > 0 && (h >> 1) <= 64) {  // small levels: wave 0 alone
+    if (tid < 64) {
+      int hh = h;
+      for (; lev < nlev && (hh >> 1) <= 64; ++lev, hh <<= 1) {
+        JWV_STAMP(2 + lev);
+        const int half = hh >> 1;
+        const bool v = tid < half;
+        const int m = v ? tid : half - 1;
+        double xe, xo;
+        if (hh < L) {
+          constexpr int HM = L / 2;
+          double av[HM], dv[HM];
+#pragma unroll
+          for (int i = 0; i < HM; ++i) {
+            av[i] = i < half ? lds[i] : 0.0;
+            dv[i] = i < half ? lds[half + i] : 0.0;
+          }
+          xe = rev_small_regs<L, FMA>(tp, av, dv, hh, 2 * m);
+          xo = rev_small_regs<L, FMA>(tp, av, dv, hh, 2 * m + 1);
+        } else {
+          rev_pair_wrap<L, FMA>(tp, lds, half, m, xe, xo);
+        }
+        wave_lds_sync();
+        if (v) *reinterpret_cast<double2*>(lds + 2 * m) = make_double2(xe, xo);
+        wave_lds_sync();
+      }
+      h = hh;
+    }
+    // the other waves catch up on (h, lev); wave 0 has already advanced
+    while ((h >> 1) <= 64 && lev < nlev) { ++lev; h <<= 1; }
+    lds_barrier();
+  }
+  for (; lev < nlev; ++lev, h <<= 1) {
+    JWV_STAMP(2 + lev);
+    const int half = h >> 1;
+    double xe[RM], xo[RM];
+    auto slot = [&](int r) { rev_pair_wrap<L, FMA>(tp, lds, half, tid + r * NT, xe[r], xo[r]); };
+    const int R = half / NT;
+    if (R <= 1) {
+      if (tid < half) slot(0);
+    } else if (R == 2) {
+#pragma unroll
+      for (int r = 0; r < 2; ++r) slot(r);
+    } else if (R == 4) {
+#pragma unroll
+      for (int r = 0; r < (RM < 4 ? RM : 4); ++r) slot(r);
+    } else if (R == 8) {
+#pragma unroll
+      for (int r = 0; r < (RM < 8 ? RM : 8); ++r) slot(r);
+    } else {
+#pragma unroll
+      for (int r = 0; r < (RM < 16 ? RM : 16); ++r) slot(r);
+    }
+    lds_barrier();
+    if (R <= 1) {
+      if (tid < half) *reinterpret_cast<double2*>(lds + 2 * tid) = make_double2(xe[0], xo[0]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < RM; ++r)
+        if (r < R) {
+          const int m = tid + r * NT;
+          *reinterpret_cast<double2*>(lds + 2 * m) = make_double2(xe[r], xo[r]);
+        }
+    }
+    lds_barrier();
+  }
+  JWV_STAMP(40);
+  double* __restrict__ y = dst + o * s_dst;
+  for (int q = 2 * tid; q < htop; q += 2 * NT)
+    *reinterpret_cast<double2*>(y + q) = *reinterpret_cast<const double2*>(lds + q);
+  JWV_STAMP(42);
+}
+
+}  // namespace jwv

@@ -228,11 +228,11 @@ __global__ __launch_bounds__(NT) void fwt_fwd_res(const double* __restrict__ src
       av[r] = a;
       if (v && c0 + c < inner) y[(int64_t)(half + i) * dv.s_len + c] = d;
     });
-    __syncthreads();
+    lds_barrier();
     for_pairs<MAXP, NT>(np, [&](int r, int p, bool v) {
       if (v) lds[p] = av[r];
     });
-    __syncthreads();
+    lds_barrier();
   }
   if (lev < nlev) {  // small levels: wave 0 only
     if (tid < 64) {
@@ -252,7 +252,7 @@ __global__ __launch_bounds__(NT) void fwt_fwd_res(const double* __restrict__ src
     }
     h >>= (nlev - lev);
     JWV_STAMP(40);
-    __syncthreads();
+    lds_barrier();
   }
   JWV_STAMP(41);
   for (int q = tid; q < h * C; q += NT) {
@@ -319,11 +319,11 @@ __global__ __launch_bounds__(NT) void fwt_fwd_tile(const double* __restrict__ sr
       av[r] = a;
       if (v && i < own && c0 + c < inner) y[(dbase + i) * dv.s_len + c] = d;
     });
-    __syncthreads();
+    lds_barrier();
     for_pairs<MAXP, NT>(np, [&](int r, int p, bool v) {
       if (v) lds[p] = av[r];
     });
-    __syncthreads();
+    lds_barrier();
     m = mo;
     hl >>= 1;
   }
@@ -395,7 +395,7 @@ __global__ __launch_bounds__(NTC + 64) void fwt_fwd_stream(
 
   if (loader && count > 0) issue(first, lds);
   if (loader) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  lds_barrier();
 
   for (int64_t k = 0; k < count; ++k) {
     const int64_t g = first + k * stride;
@@ -420,13 +420,13 @@ __global__ __launch_bounds__(NTC + 64) void fwt_fwd_stream(
           if (v && p < own) y[dbase + p] = d;
         });
       }
-      __syncthreads();
+      lds_barrier();
       if (!loader) {
         for_pairs<MAXP, NTC>(mo, [&](int r, int p, bool v) {
           if (v) cur[p] = av[r];
         });
       }
-      __syncthreads();
+      lds_barrier();
       m = mo;
       hl >>= 1;
     }
@@ -435,7 +435,7 @@ __global__ __launch_bounds__(NTC + 64) void fwt_fwd_stream(
       for (int q = tid; q < own; q += NTC) ya[(int64_t)t * own + q] = cur[q];
     if (k < 10) JWV_STAMP(3 * k + 1);
     if (loader) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // next buffer landed; this buffer free for the tile after
+    lds_barrier();  // next buffer landed; this buffer free for the tile after
     if (k < 10) JWV_STAMP(3 * k + 2);
   }
 }
@@ -478,9 +478,11 @@ __global__ __launch_bounds__(NT) void fwt_rev_res(const double* __restrict__ src
   const int tid = threadIdx.x;
   const int htop = nlev > 0 ? (h0 << (nlev - 1)) : h0;
 
+  JWV_STAMP(0);
   load_window<C, NT, MAXU>(lds, s, htop, dma != 0, c0, inner,
                            [&](int e) { return (int64_t)e * sv.s_len; });
   dma_fence_barrier();
+  JWV_STAMP(1);
 
   // one synthesis pair of a level of size h >= L, from the LDS level image
   auto pair_at = [&](int h, int p, double& xe, double& xo) {
@@ -504,8 +506,13 @@ __global__ __launch_bounds__(NT) void fwt_rev_res(const double* __restrict__ src
   int h = h0, lev = 0;
   if ((h >> 1) * C <= 64 && nlev > 0) {  // small levels: wave 0 only
     if (tid < 64) {
+#ifdef JWV_REPEAT_SMALL
+     for (int rep2 = 0; rep2 < JWV_REPEAT_SMALL; ++rep2) {
+      JWV_STAMP(44 + rep2);
+#endif
       int hh = h;
       for (int lv = 0; lv < nlev && (hh >> 1) * C <= 64; ++lv, hh <<= 1) {
+        JWV_STAMP(16 + lv);
         const int np = (hh >> 1) * C;
         const bool v = tid < np;
         const int p = v ? tid : np - 1;
@@ -519,10 +526,14 @@ __global__ __launch_bounds__(NT) void fwt_rev_res(const double* __restrict__ src
         }
         wave_lds_sync();
       }
+#ifdef JWV_REPEAT_SMALL
+     }
+#endif
     }
     while (lev < nlev && (h >> 1) * C <= 64) { ++lev; h <<= 1; }
-    __syncthreads();
+    lds_barrier();
   }
+  JWV_STAMP(2);
   // block-wide levels that still wrap several times (runtime L with C = 8:
   // h < 64 so np <= 256 = 2 slots of NT >= 128; all read before any write)
   for (; lev < nlev && h < nL; ++lev, h <<= 1) {
@@ -531,7 +542,7 @@ __global__ __launch_bounds__(NT) void fwt_rev_res(const double* __restrict__ src
 #pragma unroll
     for (int r = 0; r < 2; ++r)
       if (tid + r * NT < np) pair_small(h, tid + r * NT, xe[r], xo[r]);
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       const int p = tid + r * NT;
@@ -541,13 +552,14 @@ __global__ __launch_bounds__(NT) void fwt_rev_res(const double* __restrict__ src
         lds[(2 * m + 1) * C + c] = xo[r];
       }
     }
-    __syncthreads();
+    lds_barrier();
   }
   for (; lev < nlev; ++lev, h <<= 1) {
+    JWV_STAMP(3 + lev);
     const int np = (h >> 1) * C;
     double xe[MAXP], xo[MAXP];
     for_pairs<MAXP, NT>(np, [&](int r, int p, bool v) { pair_at(h, p, xe[r], xo[r]); });
-    __syncthreads();
+    lds_barrier();
     for_pairs<MAXP, NT>(np, [&](int r, int p, bool v) {
       if (v) {
         const int m = p / C, c = p % C;
@@ -555,12 +567,14 @@ __global__ __launch_bounds__(NT) void fwt_rev_res(const double* __restrict__ src
         lds[(2 * m + 1) * C + c] = xo[r];
       }
     });
-    __syncthreads();
+    lds_barrier();
   }
+  JWV_STAMP(30);
   for (int q = tid; q < htop * C; q += NT) {
     const int i = q / C, c = q % C;
     if (c0 + c < inner) y[(int64_t)i * dv.s_len + c] = lds[q];
   }
+  JWV_STAMP(42);
 }
 
 // ====================================================================
@@ -674,7 +688,7 @@ __global__ __launch_bounds__(NT) void fwt_rev_tile(const double* __restrict__ as
         }
       });
     } else {
-      __syncthreads();
+      lds_barrier();
       for_pairs<MAXP, NT>(np, [&](int r, int p, bool v) {
         if (v) {
           const int ml = p / C, c = p % C;
@@ -682,7 +696,7 @@ __global__ __launch_bounds__(NT) void fwt_rev_tile(const double* __restrict__ as
           abuf[(2 * ml + 1) * C + c] = xo[r];
         }
       });
-      __syncthreads();
+      lds_barrier();
     }
   }
 }

@@ -93,11 +93,23 @@ __device__ __forceinline__ void dma16_asm(const void* g, double* lds_dst) {
       : "memory", "m0");
 }
 
+// Workgroup barrier that orders LDS only.  __syncthreads() is a workgroup
+// fence on every address space: the compiler puts `s_waitcnt vmcnt(0)` in
+// front of it, so each barrier would wait until the wave's global stores
+// (detail coefficients already on their way to HBM) are acknowledged.  None
+// of these kernels reads global memory written in the same launch, so an
+// LDS-scoped fence (lgkmcnt only) is the complete requirement.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // Wait for this wave's LDS-DMA loads, then a workgroup barrier: after it
 // every wave sees every other wave's DMA'd rows in LDS.
 __device__ __forceinline__ void dma_fence_barrier() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  lds_barrier();
 }
 
 // Load a window of W rows (C doubles each; row e from global src + rowoff(e),
@@ -177,9 +189,9 @@ __device__ __forceinline__ void for_pairs(int np, F&& f) {
 // Wave-local LDS ordering: a wave's LDS ops execute in program order, so only
 // the compiler has to be kept from moving them across this point.
 __device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
 }
 
 template <bool FMA>

@@ -79,14 +79,14 @@ struct Geo {
   static bool fwd_stream();          // env JWV_FWD_STREAM (default 0)
   static int stream_blocks_per_cu(); // env JWV_STREAM_BPC (default 2)
   static int stream_ntc();           // env JWV_STREAM_NTC: 256 | 512 (default 512)
-  // C = 1 compile-time-geometry tile kernels (fwt1_kernels.hpp): env JWV_FWT1
-  // (default 1); Daubechies4-size (L = 8) tuning variants JWV_FWD1_T (4096 |
-  // 2048), JWV_FWD1_NT (256 | 512), JWV_REV1_T (2048 | 4096), JWV_REV1_NT (256 | 128)
+  // C = 1 compile-time-geometry kernels (fwt1_kernels.hpp, fwt1_res.hpp):
+  // env JWV_FWT1 (default 1).  Tiles: forward T = 4096, reverse T = 2048, up
+  // to kFwt1KMax fused levels; the planner lets the last forward tile pass run
+  // down to kFwt1Tail samples and starts the reverse tile passes above
+  // kFwt1Tail * 2, so the single-block tails stay short.
   static bool fwt1();
-  static int fwd1_t();
-  static int fwd1_nt();
-  static int rev1_t();
-  static int rev1_nt();
+  static constexpr int kFwt1T = 4096, kRev1T = 2048, kFwt1KMax = 9;
+  static constexpr int kFwt1FwdTail = 512, kFwt1RevTail = 1024;
   static int fwt_t(int C) { return C == 1 ? kFwtT1 : kFwtT8; }
   static int fwt_k(int C) { return C == 1 ? kFwtK1 : kFwtK8; }
   static int wpt_t(int C) { return C == 1 ? kWptT1 : kWptT8; }
@@ -113,6 +113,8 @@ hipError_t launch_copy_axis(const double* src, AxisView sv, double* dst, AxisVie
 // twice (JWV_FMA=0 / 1).
 namespace exact {
 // fwt1 kernels: return false when the case is not covered (nothing launched)
+bool fwt_fwd_res1(const Bank&, const ResArgs&, hipStream_t, hipError_t& err);
+bool fwt_rev_res1(const Bank&, const ResArgs&, hipStream_t, hipError_t& err);
 bool fwt_fwd_tile1(const Bank&, const TileArgs&, hipStream_t, hipError_t& err);
 bool fwt_rev_tile1(const Bank&, const TileArgs&, hipStream_t, hipError_t& err);
 hipError_t fwt_fwd_res(const Bank&, int C, const ResArgs&, hipStream_t);
@@ -128,6 +130,8 @@ hipError_t modwt_inv(const Bank&, bool tiled, const ModwtArgs&, hipStream_t);
 }  // namespace exact
 namespace fused {
 // fwt1 kernels: return false when the case is not covered (nothing launched)
+bool fwt_fwd_res1(const Bank&, const ResArgs&, hipStream_t, hipError_t& err);
+bool fwt_rev_res1(const Bank&, const ResArgs&, hipStream_t, hipError_t& err);
 bool fwt_fwd_tile1(const Bank&, const TileArgs&, hipStream_t, hipError_t& err);
 bool fwt_rev_tile1(const Bank&, const TileArgs&, hipStream_t, hipError_t& err);
 hipError_t fwt_fwd_res(const Bank&, int C, const ResArgs&, hipStream_t);

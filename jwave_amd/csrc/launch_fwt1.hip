@@ -3,6 +3,7 @@
 // launch_fwt_wpt.hip).  Used for contiguous, 16-B aligned signals with a
 // compiled-in tap count; every other case keeps the generic tile kernels.
 #include "fwt1_kernels.hpp"
+#include "fwt1_res.hpp"
 #include "jwv_launch.hpp"
 
 #ifndef JWV_FMA
@@ -17,6 +18,7 @@
 namespace jwv {
 namespace {
 constexpr bool kFMA = JWV_FMA != 0;
+constexpr int kFwdT = Geo::kFwt1T, kRevT = Geo::kRev1T;
 
 template <typename Kern>
 hipError_t prep1(Kern kernel, size_t lds) {
@@ -38,24 +40,20 @@ hipError_t fwd1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
                      a.av.s_outer, a.h, tp);
   return hipGetLastError();
 }
-template <int L, int NT, int T>
-hipError_t fwd1_t(const Bank& b, const TileArgs& a, hipStream_t s) {
+template <int L>
+hipError_t fwd1_l(const Bank& b, const TileArgs& a, hipStream_t s) {
+  constexpr int NT = 256, T = kFwdT;
   switch (a.K) {
     case 1: return fwd1_k<L, NT, T, 1>(b, a, s);
     case 2: return fwd1_k<L, NT, T, 2>(b, a, s);
     case 3: return fwd1_k<L, NT, T, 3>(b, a, s);
     case 4: return fwd1_k<L, NT, T, 4>(b, a, s);
     case 5: return fwd1_k<L, NT, T, 5>(b, a, s);
-    default: return fwd1_k<L, NT, T, 6>(b, a, s);
+    case 6: return fwd1_k<L, NT, T, 6>(b, a, s);
+    case 7: return fwd1_k<L, NT, T, 7>(b, a, s);
+    case 8: return fwd1_k<L, NT, T, 8>(b, a, s);
+    default: return fwd1_k<L, NT, T, 9>(b, a, s);
   }
-}
-template <int L>
-hipError_t fwd1_l(const Bank& b, const TileArgs& a, hipStream_t s) {
-  if constexpr (L == 8) {  // geometry variants for tuning (env JWV_FWD1_T / JWV_FWD1_NT)
-    if (Geo::fwd1_t() == 2048) return fwd1_t<L, 256, 2048>(b, a, s);
-    if (Geo::fwd1_nt() == 512) return fwd1_t<L, 512, 4096>(b, a, s);
-  }
-  return fwd1_t<L, 256, 4096>(b, a, s);
 }
 
 template <int L, int NT, int T, int K>
@@ -71,24 +69,48 @@ hipError_t rev1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
                      a.dv.s_outer, hK, tp);
   return hipGetLastError();
 }
-template <int L, int NT, int T>
-hipError_t rev1_t(const Bank& b, const TileArgs& a, hipStream_t s) {
+template <int L>
+hipError_t rev1_l(const Bank& b, const TileArgs& a, hipStream_t s) {
+  constexpr int NT = 256, T = kRevT;
   switch (a.K) {
     case 1: return rev1_k<L, NT, T, 1>(b, a, s);
     case 2: return rev1_k<L, NT, T, 2>(b, a, s);
     case 3: return rev1_k<L, NT, T, 3>(b, a, s);
     case 4: return rev1_k<L, NT, T, 4>(b, a, s);
     case 5: return rev1_k<L, NT, T, 5>(b, a, s);
-    default: return rev1_k<L, NT, T, 6>(b, a, s);
+    case 6: return rev1_k<L, NT, T, 6>(b, a, s);
+    case 7: return rev1_k<L, NT, T, 7>(b, a, s);
+    case 8: return rev1_k<L, NT, T, 8>(b, a, s);
+    default: return rev1_k<L, NT, T, 9>(b, a, s);
   }
 }
+
+// resident kernels for a handful of rows (latency-bound tail): 1024 threads
+constexpr int kCap = Geo::kResCap1;
 template <int L>
-hipError_t rev1_l(const Bank& b, const TileArgs& a, hipStream_t s) {
-  if constexpr (L == 8) {  // env JWV_REV1_T / JWV_REV1_NT
-    if (Geo::rev1_t() == 4096) return rev1_t<L, 256, 4096>(b, a, s);
-    if (Geo::rev1_nt() == 128) return rev1_t<L, 128, 2048>(b, a, s);
-  }
-  return rev1_t<L, 256, 2048>(b, a, s);
+hipError_t fwd_res1_l(const Bank& b, const ResArgs& a, hipStream_t s) {
+  FwdTaps<L> tp;
+  for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
+  const size_t lds = (size_t)(a.n + 2) * sizeof(double);
+  const dim3 grid((unsigned)a.nouter);
+  auto k = fwt_fwd_res1<L, 1024, kCap, kFMA>;
+  if (hipError_t e = prep1(k, lds)) return e;
+  hipLaunchKernelGGL(k, grid, dim3(1024), lds, s, a.src, a.sv.s_outer, a.dst, a.dv.s_outer, a.n,
+                     a.nlev, tp);
+  return hipGetLastError();
+}
+template <int L>
+hipError_t rev_res1_l(const Bank& b, const ResArgs& a, hipStream_t s) {
+  RevTaps<L> tp;
+  for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
+  const int htop = a.nlev > 0 ? (a.n << (a.nlev - 1)) : a.n;
+  const size_t lds = (size_t)(htop + 2) * sizeof(double);
+  const dim3 grid((unsigned)a.nouter);
+  auto k = fwt_rev_res1<L, 1024, kCap, kFMA>;
+  if (hipError_t e = prep1(k, lds)) return e;
+  hipLaunchKernelGGL(k, grid, dim3(1024), lds, s, a.src, a.sv.s_outer, a.dst, a.dv.s_outer, a.n,
+                     a.nlev, tp);
+  return hipGetLastError();
 }
 
 bool plain(const AxisView& v) { return v.pk == 1 && v.s_len == 1; }
@@ -98,9 +120,9 @@ bool even_rows(const AxisView& v, int64_t nouter) { return nouter == 1 || (v.s_o
 namespace JWV_NS {
 // Returns false (and launches nothing) when the case is not covered.
 bool fwt_fwd_tile1(const Bank& b, const TileArgs& a, hipStream_t s, hipError_t& err) {
-  if (!Geo::fwt1() || !a.dma || a.inner != 1 || b.scale != 1.0) return false;
-  if (!plain(a.sv) || !plain(a.dv) || !plain(a.av) || a.K < 1 || a.K > 6) return false;
-  if (a.h % 4096) return false;
+  if (!Geo::fwt1() || !a.dma || a.inner != 1) return false;  // (scale: synthesis only)
+  if (!plain(a.sv) || !plain(a.dv) || !plain(a.av) || a.K < 1 || a.K > Geo::kFwt1KMax) return false;
+  if (a.h % kFwdT) return false;
   switch (b.L) {
     case 2: err = fwd1_l<2>(b, a, s); return true;
     case 4: err = fwd1_l<4>(b, a, s); return true;
@@ -109,11 +131,39 @@ bool fwt_fwd_tile1(const Bank& b, const TileArgs& a, hipStream_t s, hipError_t& 
     default: return false;
   }
 }
+// Only for a handful of signals (the latency-bound tail of long 1-D signals):
+// batches of rows keep the generic resident kernels (higher occupancy).
+bool fwt_fwd_res1(const Bank& b, const ResArgs& a, hipStream_t s, hipError_t& err) {
+  if (!Geo::fwt1() || !a.dma || a.inner != 1 || !plain(a.sv) || !plain(a.dv)) return false;
+  if (a.nouter >= 64) return false;
+  if (a.n > kCap || a.n < 2) return false;
+  switch (b.L) {
+    case 2: err = fwd_res1_l<2>(b, a, s); return true;
+    case 4: err = fwd_res1_l<4>(b, a, s); return true;
+    case 8: err = fwd_res1_l<8>(b, a, s); return true;
+    case 16: err = fwd_res1_l<16>(b, a, s); return true;
+    default: return false;
+  }
+}
+bool fwt_rev_res1(const Bank& b, const ResArgs& a, hipStream_t s, hipError_t& err) {
+  if (!Geo::fwt1() || !a.dma || a.inner != 1 || b.scale != 1.0) return false;
+  if (!plain(a.sv) || !plain(a.dv) || a.nouter >= 64) return false;
+  if (((uintptr_t)a.dst & 15) || !even_rows(a.dv, a.nouter)) return false;
+  const int64_t htop = a.nlev > 0 ? ((int64_t)a.n << (a.nlev - 1)) : a.n;
+  if (htop > kCap || htop < 2) return false;
+  switch (b.L) {
+    case 2: err = rev_res1_l<2>(b, a, s); return true;
+    case 4: err = rev_res1_l<4>(b, a, s); return true;
+    case 8: err = rev_res1_l<8>(b, a, s); return true;
+    case 16: err = rev_res1_l<16>(b, a, s); return true;
+    default: return false;
+  }
+}
 bool fwt_rev_tile1(const Bank& b, const TileArgs& a, hipStream_t s, hipError_t& err) {
   if (!Geo::fwt1() || !a.dma || a.inner != 1 || b.scale != 1.0) return false;
-  if (!plain(a.sv) || !plain(a.cv) || !plain(a.dv) || a.K < 1 || a.K > 6) return false;
+  if (!plain(a.sv) || !plain(a.cv) || !plain(a.dv) || a.K < 1 || a.K > Geo::kFwt1KMax) return false;
   if (((uintptr_t)a.dst & 15) || !even_rows(a.dv, a.nouter)) return false;
-  if ((a.h << (a.K - 1)) % 4096) return false;
+  if ((a.h << (a.K - 1)) % kRevT) return false;
   switch (b.L) {
     case 2: err = rev1_l<2>(b, a, s); return true;
     case 4: err = rev1_l<4>(b, a, s); return true;

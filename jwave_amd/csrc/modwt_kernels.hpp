@@ -64,7 +64,7 @@ __global__ __launch_bounds__(NT) void modwt_fwd_tile(const double* __restrict__ 
   const int W = T + S;
   load_window<1, NT, MAXP>(lds, src, W, false, 0, 1,
                            [&](int e) { return wrap_mod(t0 - S + e, N); });
-  __syncthreads();
+  lds_barrier();
   int Sj = S;  // halo still carried by the level input
   for (int j = j0; j <= j1; ++j) {
     const int st = 1 << (j - 1);
@@ -90,13 +90,13 @@ __global__ __launch_bounds__(NT) void modwt_fwd_tile(const double* __restrict__ 
         if (e >= S && g < N) wrow[g] = sw;
       }
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int r = 0; r < MAXP; ++r) {
       const int p = tid + r * NT;
       if (p < nout) lds[e0 + p] = vv[r];
     }
-    __syncthreads();
+    lds_barrier();
     Sj = Sn;
   }
   for (int p = tid; p < T; p += NT) {
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(NT) void modwt_inv_tile(const double* __restrict__ 
     const double* wrow = coef + (int64_t)(j - 1) * ldw;
     load_window<1, NT, MAXP>(wb, wrow, T + Rj, false, 0, 1,
                              [&](int e) { return wrap_mod(t0 + e, N); });
-    __syncthreads();
+    lds_barrier();
     const int nout = T + Rn;
     double vv[MAXP];
 #pragma unroll
@@ -165,7 +165,7 @@ __global__ __launch_bounds__(NT) void modwt_inv_tile(const double* __restrict__ 
         vv[r] = sa + sd;
       }
     }
-    __syncthreads();
+    lds_barrier();
     if (j == j0) {
 #pragma unroll
       for (int r = 0; r < MAXP; ++r) {
@@ -178,7 +178,7 @@ __global__ __launch_bounds__(NT) void modwt_inv_tile(const double* __restrict__ 
         const int p = tid + r * NT;
         if (p < nout) vb[p] = vv[r];
       }
-      __syncthreads();
+      lds_barrier();
     }
     Rj = Rn;
   }

@@ -52,7 +52,7 @@ __global__ __launch_bounds__(NT) void wpt_fwd_res(const double* __restrict__ src
                          av[r], dv2[r]);
       }
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int r = 0; r < MAXP; ++r) {
       const int p = tid + r * NT;
@@ -63,7 +63,7 @@ __global__ __launch_bounds__(NT) void wpt_fwd_res(const double* __restrict__ src
         lds[(pk * h + half + i) * C + c] = dv2[r];
       }
     }
-    __syncthreads();
+    lds_barrier();
     h = half;
   }
   for (int q = tid; q < n * C; q += NT) {
@@ -120,7 +120,7 @@ __global__ __launch_bounds__(NT) void wpt_fwd_tile(const double* __restrict__ sr
                          dv2[r]);
       }
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int r = 0; r < MAXP; ++r) {
       const int p = tid + r * NT;
@@ -131,7 +131,7 @@ __global__ __launch_bounds__(NT) void wpt_fwd_tile(const double* __restrict__ sr
         lds[((2 * f + 1) * mo + i) * C + c] = dv2[r];
       }
     }
-    __syncthreads();
+    lds_barrier();
     m = mo;
   }
   // 2^K bands, own part T>>K of each
@@ -192,7 +192,7 @@ __global__ __launch_bounds__(NT) void wpt_rev_res(const double* __restrict__ src
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int r = 0; r < MAXP; ++r) {
       const int p = tid + r * NT;
@@ -203,7 +203,7 @@ __global__ __launch_bounds__(NT) void wpt_rev_res(const double* __restrict__ src
         lds[(pk * h + 2 * m + 1) * C + c] = xo[r];
       }
     }
-    __syncthreads();
+    lds_barrier();
     h <<= 1;
   }
   for (int q = tid; q < n * C; q += NT) {
@@ -300,7 +300,7 @@ __global__ __launch_bounds__(NT) void wpt_rev_tile(const double* __restrict__ sr
         }
       }
     } else {
-      __syncthreads();
+      lds_barrier();
 #pragma unroll
       for (int r = 0; r < MAXP; ++r) {
         const int p = tid + r * NT;
@@ -311,7 +311,7 @@ __global__ __launch_bounds__(NT) void wpt_rev_tile(const double* __restrict__ sr
           lds[(f * Wl + 2 * ml + 1) * C + c] = xo[r];
         }
       }
-      __syncthreads();
+      lds_barrier();
     }
   }
 }
