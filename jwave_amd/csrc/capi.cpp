@@ -234,7 +234,8 @@ bool fast1(const Bank& b, const Axis& a, bool rev) {
   if (rev && b.scale != 1.0) return false;
   if (a.sv.pk != 1 || a.dv.pk != 1 || a.sv.s_len != 1 || a.dv.s_len != 1) return false;
   if (!dma_view(a.src, a.sv, 1, 1)) return false;
-  if (rev && (((uintptr_t)a.dst & 15) || (a.outer > 1 && (a.dv.s_outer & 1)))) return false;
+  // 16-B output stores (both directions)
+  if (((uintptr_t)a.dst & 15) || (a.outer > 1 && (a.dv.s_outer & 1))) return false;
   return true;
 }
 

@@ -7,8 +7,9 @@
 // Same math and summation order as fwt_fwd_tile / fwt_rev_tile
 // (Wavelet.java:236-303; see fwt_kernels.hpp), so EXACT results stay
 // bit-identical.  Differences are structural only:
-//  * levels ping-pong between two LDS buffers: one barrier per level and no
-//    per-slot result registers held across a barrier;
+//  * reverse levels ping-pong between two LDS buffers (one barrier per
+//    level); the forward runs level 1 in place and ping-pongs the rest inside
+//    the level-0 window (LDS = one window);
 //  * detail / output stores use an SGPR base + 32-bit lane offset; the final
 //    synthesis level stores (x[2m], x[2m+1]) as one 16-B store;
 //  * reverse: the array-head pairs (Wavelet.java:284-296 wrap order) exist
@@ -20,43 +21,80 @@ namespace jwv {
 
 // ---------------------------------------------------------------- forward
 // Window after l fused levels: T/2^l own samples + (L-2)(2^(K-l) - 1) halo.
+// LDS holds only the level-0 window: level 1 runs in place (its results wait
+// in registers across one extra barrier), then levels alternate between
+// offset 0 (odd l) and offset o2 = even(m(1)) (even l) inside that window.
 template <int L, int T, int K>
 struct Fwd1Geo {
   static constexpr int m(int l) { return (T >> l) + (L - 2) * ((1 << (K - l)) - 1); }
-  static constexpr int buf0() { return (m(0) + 2) & ~1; }  // + DMA overrun, even
-  static constexpr int lds_doubles() { return buf0() + ((m(1) + 1) & ~1); }
+  static constexpr int o2() { return (m(1) + 1) & ~1; }
+  static_assert((L & 1) == 0 && ((T >> K) & 1) == 0, "pair couples need even windows");
+  static constexpr int off(int l) { return (l & 1) ? 0 : o2(); }  // level-l output (l >= 1)
+  static constexpr int lds_doubles() {
+    return (m(0) + 2 > o2() + m(2 <= K ? 2 : 1)) ? m(0) + 2 : o2() + m(2 <= K ? 2 : 1);
+  }
 };
 
 template <int L, int NT, int T, int K, bool FMA, int l>
 struct Fwd1Level {
-  // in: level-(l-1) window (m(l-1) samples); out: level-l approximation window.
-  // yd: this tile's first detail of level l; ya: first level-K approximation.
-  __device__ __forceinline__ static void run(const FwdTaps<L>& tp, const double* in, double* out,
+  // level l reads the level-(l-1) window at lds + off(l-1) (l = 1: lds) and
+  // writes its approximations at lds + off(l) (the last level: ya).
+  // yd0: the signal's coefficient row; ya: its level-K approximation row.
+  // Each lane computes two adjacent pairs (p, p+1): one 16-B store per lane
+  // for the details and approximations, L+2 window reads for two pairs.
+  __device__ __forceinline__ static void run(const FwdTaps<L>& tp, double* lds,
                                              double* __restrict__ yd0, int hl, int t,
                                              double* __restrict__ ya) {
     using G = Fwd1Geo<L, T, K>;
-    constexpr int mo = G::m(l);
-    constexpr int own = T >> l;
-    constexpr int R = (mo + NT - 1) / NT;
+    constexpr int mo = G::m(l);      // even
+    constexpr int own = T >> l;      // even
+    constexpr int NP2 = mo / 2;      // pair couples
+    constexpr int R = (NP2 + NT - 1) / NT;
+    const double* in = lds + (l == 1 ? 0 : G::off(l - 1));
+    double* out = lds + G::off(l);
     const int tid = threadIdx.x;
     double* __restrict__ yd = yd0 + (hl >> 1) + (int64_t)t * own;
+    double2 av[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const int p = tid + r * NT;
-      if ((r + 1) * NT <= mo || p < mo) {
-        double a, d;
-        fwd_pair<L, FMA>(tp, [&](int j) { return in[2 * p + j]; }, a, d);
-        if constexpr (l == K) {
-          ya[(int64_t)t * own + p] = a;  // mo == own at the last level
-        } else {
-          out[p] = a;
+      const int q = tid + r * NT;  // couple index: pairs 2q, 2q+1
+      if ((r + 1) * NT <= NP2 || q < NP2) {
+        double x[L + 2];
+#pragma unroll
+        for (int j = 0; j < L + 2; j += 2) {
+          const double2 v = *reinterpret_cast<const double2*>(in + 4 * q + j);
+          x[j] = v.x;
+          x[j + 1] = v.y;
         }
-        if (r * NT < own && ((r + 1) * NT <= own || p < own)) yd[p] = d;
+        double a0, d0, a1, d1;
+        fwd_pair<L, FMA>(tp, [&](int j) { return x[j]; }, a0, d0);
+        fwd_pair<L, FMA>(tp, [&](int j) { return x[j + 2]; }, a1, d1);
+        const int p = 2 * q;
+        if constexpr (l == K) {
+          *reinterpret_cast<double2*>(ya + (int64_t)t * own + p) = make_double2(a0, a1);
+        } else if constexpr (l == 1) {
+          av[r] = make_double2(a0, a1);  // in place: written after every wave has read
+        } else {
+          *reinterpret_cast<double2*>(out + p) = make_double2(a0, a1);
+        }
+#ifdef JWV_EXP_NOSTORE_DEEP  // diagnostic builds only
+        if (l == 1)
+#endif
+        if (2 * r * NT < own && (2 * (r + 1) * NT <= own || p < own))
+          *reinterpret_cast<double2*>(yd + p) = make_double2(d0, d1);
       }
     }
     if constexpr (l < K) {
+      if constexpr (l == 1) {
+        lds_barrier();
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int q = tid + r * NT;
+          if ((r + 1) * NT <= NP2 || q < NP2) *reinterpret_cast<double2*>(out + 2 * q) = av[r];
+        }
+      }
       lds_barrier();
-      Fwd1Level<L, NT, T, K, FMA, l + 1>::run(tp, out, const_cast<double*>(in), yd0, hl >> 1, t, ya);
+      Fwd1Level<L, NT, T, K, FMA, l + 1>::run(tp, lds, yd0, hl >> 1, t, ya);
     }
   }
 };
@@ -83,8 +121,7 @@ __global__ __launch_bounds__(NT) void fwt_fwd_tile1(const double* __restrict__ s
   load_window<1, NT, (M0 + NT - 1) / NT>(lds, s, M0, true, 0, 1,
                                           [&](int e) { return (int64_t)((base + e) & msk); });
   dma_fence_barrier();
-  Fwd1Level<L, NT, T, K, FMA, 1>::run(tp, lds, lds + G::buf0(), dst + o * s_dst, h, t,
-                                      adst + o * s_adst);
+  Fwd1Level<L, NT, T, K, FMA, 1>::run(tp, lds, dst + o * s_dst, h, t, adst + o * s_adst);
 }
 
 // ---------------------------------------------------------------- reverse

@@ -85,7 +85,7 @@ struct Geo {
   // down to kFwt1Tail samples and starts the reverse tile passes above
   // kFwt1Tail * 2, so the single-block tails stay short.
   static bool fwt1();
-  static constexpr int kFwt1T = 4096, kRev1T = 2048, kFwt1KMax = 9;
+  static constexpr int kFwt1T = 2048, kRev1T = 2048, kFwt1KMax = 9;
   static constexpr int kFwt1FwdTail = 512, kFwt1RevTail = 1024;
   static int fwt_t(int C) { return C == 1 ? kFwtT1 : kFwtT8; }
   static int fwt_k(int C) { return C == 1 ? kFwtK1 : kFwtK8; }

@@ -122,6 +122,9 @@ namespace JWV_NS {
 bool fwt_fwd_tile1(const Bank& b, const TileArgs& a, hipStream_t s, hipError_t& err) {
   if (!Geo::fwt1() || !a.dma || a.inner != 1) return false;  // (scale: synthesis only)
   if (!plain(a.sv) || !plain(a.dv) || !plain(a.av) || a.K < 1 || a.K > Geo::kFwt1KMax) return false;
+  if (((uintptr_t)a.dst & 15) || ((uintptr_t)a.adst & 15) || !even_rows(a.dv, a.nouter) ||
+      !even_rows(a.av, a.nouter))
+    return false;
   if (a.h % kFwdT) return false;
   switch (b.L) {
     case 2: err = fwd1_l<2>(b, a, s); return true;
