@@ -420,11 +420,40 @@ void wpt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
   run_wpt_passes(c, b, a, true, ps);
 }
 
+// wpt1 kernels (launch_fwt1.hip) take every tiled WPT pass of this axis:
+// contiguous 16-B aligned rows and packets, compiled-in tap count, unscaled
+// synthesis bank (mirrors wpt_tile1's checks).
+bool fastw(const Bank& b, const Axis& a, bool rev) {
+  if (!Geo::fwt1() || a.inner != 1 || jwv::static_l(b.L) == 0) return false;
+  if (rev && b.scale != 1.0) return false;
+  if (a.sv.s_len != 1 || a.dv.s_len != 1 || (a.sv.s_outer & 1) || (a.dv.s_outer & 1)) return false;
+  if (((uintptr_t)a.src & 15) || ((uintptr_t)a.dst & 15)) return false;
+  return true;
+}
+
 void wpt_rev_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
   const int h = rev_first(a.len, b.tw, level);
   if (h == 0) return copy_axis(c, a);
   const int C = col_slab(a.inner), cap = Geo::res_cap(C), KM = Geo::wpt_k(C);
   std::vector<WPass> ps;
+  if (fastw(b, a, true) && a.len >= Geo::kWpt1T) {
+    // passes from the top: K = min(levels left, kWpt1KMax) ending at packet
+    // size hK while hK >= the tile; the rest (packets < tile <= cap) resident
+    std::vector<WPass> top;
+    int nl = exponent(a.len / h) + 1, hK = a.len;
+    while (nl > 0) {
+      if (hK < Geo::kWpt1T) {
+        top.push_back({false, hK, h, nl, a.len / hK});
+        break;
+      }
+      const int K = std::min(nl, Geo::kWpt1KMax);
+      top.push_back({true, hK, 0, K, a.len / hK});
+      nl -= K;
+      hK >>= K;
+    }
+    ps.assign(top.rbegin(), top.rend());
+    return run_wpt_passes(c, b, a, false, ps);
+  }
   int h1;
   if (h <= cap) {
     const int hres = std::min(a.len, cap);
@@ -735,9 +764,17 @@ hipError_t launch_wpt_rev_res(const Bank& b, bool fma, int C, const ResArgs& a, 
   JWV_MODE2(wpt_rev_res, b, C, a, s);
 }
 hipError_t launch_wpt_fwd_tile(const Bank& b, bool fma, int C, const TileArgs& a, hipStream_t s) {
+  hipError_t e = hipSuccess;
+  if (C == 1 && (fma ? fused::wpt_tile1(b, a, s, true, e) : exact::wpt_tile1(b, a, s, true, e)))
+    return e;
+  if (a.K > Geo::wpt_k(C) || a.h < Geo::wpt_t(C)) return hipErrorInvalidValue;
   JWV_MODE2(wpt_fwd_tile, b, C, a, s);
 }
 hipError_t launch_wpt_rev_tile(const Bank& b, bool fma, int C, const TileArgs& a, hipStream_t s) {
+  hipError_t e = hipSuccess;
+  if (C == 1 && (fma ? fused::wpt_tile1(b, a, s, false, e) : exact::wpt_tile1(b, a, s, false, e)))
+    return e;
+  if (a.K > Geo::wpt_k(C) || a.h < Geo::wpt_t(C)) return hipErrorInvalidValue;
   JWV_MODE2(wpt_rev_tile, b, C, a, s);
 }
 hipError_t launch_modwt_fwd(const Bank& b, bool fma, bool tiled, const ModwtArgs& a,

@@ -52,7 +52,7 @@ struct Fwd1Level {
     constexpr int R = (NP2 + NT - 1) / NT;
     const double* in = lds + (l == 1 ? 0 : G::off(l - 1));
     double* out = lds + G::off(l);
-    const int tid = threadIdx.x;
+    const int tid = opaque_tid();  // per-level: keeps address math out of the prologue
     double* __restrict__ yd = yd0 + (hl >> 1) + (int64_t)t * own;
     double2 av[R];
 #pragma unroll
@@ -166,7 +166,7 @@ struct Rev1Level {
     const double* ab = lds + ((((l + 1) & 1) != 0) ? G::buf1() : G::buf0());
     const double* db = lds + G::doff(l);
     double* ob = lds + (((l & 1) != 0) ? G::buf1() : G::buf0());
-    const int tid = threadIdx.x;
+    const int tid = opaque_tid();  // per-level: keeps address math out of the prologue
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int ml = tid + r * NT;

@@ -194,6 +194,17 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
 }
 
+// threadIdx.x through an empty asm: computations derived from it cannot be
+// hoisted above this point.  The level functions of the compile-time-geometry
+// kernels take their lane index this way; otherwise the compiler hoists every
+// level's slot addresses to kernel entry and keeps them live (WPT L=16: ~200
+// VGPRs instead of ~100).
+__device__ __forceinline__ int opaque_tid() {
+  int t = (int)threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
 template <bool FMA>
 __device__ __forceinline__ double mac(double acc, double a, double b) {
   if constexpr (FMA) {

@@ -87,6 +87,7 @@ struct Geo {
   static bool fwt1();
   static constexpr int kFwt1T = 2048, kRev1T = 2048, kFwt1KMax = 9;
   static constexpr int kFwt1FwdTail = 512, kFwt1RevTail = 1024;
+  static constexpr int kWpt1T = 4096, kWpt1KMax = 6;  // WPT tiles (wpt1_kernels.hpp)
   static int fwt_t(int C) { return C == 1 ? kFwtT1 : kFwtT8; }
   static int fwt_k(int C) { return C == 1 ? kFwtK1 : kFwtK8; }
   static int wpt_t(int C) { return C == 1 ? kWptT1 : kWptT8; }
@@ -113,6 +114,7 @@ hipError_t launch_copy_axis(const double* src, AxisView sv, double* dst, AxisVie
 // twice (JWV_FMA=0 / 1).
 namespace exact {
 // fwt1 kernels: return false when the case is not covered (nothing launched)
+bool wpt_tile1(const Bank&, const TileArgs&, hipStream_t, bool fwd, hipError_t& err);
 bool fwt_fwd_res1(const Bank&, const ResArgs&, hipStream_t, hipError_t& err);
 bool fwt_rev_res1(const Bank&, const ResArgs&, hipStream_t, hipError_t& err);
 bool fwt_fwd_tile1(const Bank&, const TileArgs&, hipStream_t, hipError_t& err);
@@ -130,6 +132,7 @@ hipError_t modwt_inv(const Bank&, bool tiled, const ModwtArgs&, hipStream_t);
 }  // namespace exact
 namespace fused {
 // fwt1 kernels: return false when the case is not covered (nothing launched)
+bool wpt_tile1(const Bank&, const TileArgs&, hipStream_t, bool fwd, hipError_t& err);
 bool fwt_fwd_res1(const Bank&, const ResArgs&, hipStream_t, hipError_t& err);
 bool fwt_rev_res1(const Bank&, const ResArgs&, hipStream_t, hipError_t& err);
 bool fwt_fwd_tile1(const Bank&, const TileArgs&, hipStream_t, hipError_t& err);

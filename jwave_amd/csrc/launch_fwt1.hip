@@ -4,6 +4,7 @@
 // compiled-in tap count; every other case keeps the generic tile kernels.
 #include "fwt1_kernels.hpp"
 #include "fwt1_res.hpp"
+#include "wpt1_kernels.hpp"
 #include "jwv_launch.hpp"
 
 #ifndef JWV_FMA
@@ -113,7 +114,47 @@ hipError_t rev_res1_l(const Bank& b, const ResArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ---- WPT
+constexpr int kWptT = Geo::kWpt1T;
+template <int L, int K>
+hipError_t wfwd1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
+  auto k = wpt_fwd_tile1<L, 256, kWptT, K, kFMA>;
+  const size_t lds = (size_t)Wpt1FwdGeo<L, kWptT, K>::lds_doubles() * sizeof(double);
+  if (hipError_t e = prep1(k, lds)) return e;
+  FwdTaps<L> tp;
+  for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
+  const dim3 grid((unsigned)(a.nouter * (a.h / kWptT)));
+  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a.src, a.sv, a.dst, a.dv, a.h, tp);
+  return hipGetLastError();
+}
+template <int L, int K>
+hipError_t wrev1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
+  auto k = wpt_rev_tile1<L, 256, kWptT, K, kFMA>;
+  const size_t lds = (size_t)Wpt1RevGeo<L, kWptT, K>::lds_doubles() * sizeof(double);
+  if (hipError_t e = prep1(k, lds)) return e;
+  RevTaps<L> tp;
+  for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
+  const dim3 grid((unsigned)(a.nouter * (a.h / kWptT)));
+  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a.src, a.sv, a.dst, a.dv, a.h, tp);
+  return hipGetLastError();
+}
+template <int L>
+hipError_t wpt1_l(const Bank& b, const TileArgs& a, hipStream_t s, bool fwd) {
+  switch (a.K) {
+    case 1: return fwd ? wfwd1_k<L, 1>(b, a, s) : wrev1_k<L, 1>(b, a, s);
+    case 2: return fwd ? wfwd1_k<L, 2>(b, a, s) : wrev1_k<L, 2>(b, a, s);
+    case 3: return fwd ? wfwd1_k<L, 3>(b, a, s) : wrev1_k<L, 3>(b, a, s);
+    case 4: return fwd ? wfwd1_k<L, 4>(b, a, s) : wrev1_k<L, 4>(b, a, s);
+    case 5: return fwd ? wfwd1_k<L, 5>(b, a, s) : wrev1_k<L, 5>(b, a, s);
+    default: return fwd ? wfwd1_k<L, 6>(b, a, s) : wrev1_k<L, 6>(b, a, s);
+  }
+}
+
 bool plain(const AxisView& v) { return v.pk == 1 && v.s_len == 1; }
+// packet views: stride-1 samples, even strides (16-B aligned packet rows)
+bool pk_ok(const AxisView& v) {
+  return v.s_len == 1 && (v.s_outer & 1) == 0 && (v.pk == 1 || (v.s_pk & 1) == 0);
+}
 bool even_rows(const AxisView& v, int64_t nouter) { return nouter == 1 || (v.s_outer & 1) == 0; }
 }  // namespace
 
@@ -159,6 +200,18 @@ bool fwt_rev_res1(const Bank& b, const ResArgs& a, hipStream_t s, hipError_t& er
     case 4: err = rev_res1_l<4>(b, a, s); return true;
     case 8: err = rev_res1_l<8>(b, a, s); return true;
     case 16: err = rev_res1_l<16>(b, a, s); return true;
+    default: return false;
+  }
+}
+bool wpt_tile1(const Bank& b, const TileArgs& a, hipStream_t s, bool fwd, hipError_t& err) {
+  if (!Geo::fwt1() || !a.dma || a.inner != 1 || (!fwd && b.scale != 1.0)) return false;
+  if (!pk_ok(a.sv) || !pk_ok(a.dv) || a.K < 1 || a.K > Geo::kWpt1KMax) return false;
+  if (((uintptr_t)a.dst & 15) || ((uintptr_t)a.src & 15) || a.h < kWptT || a.h % kWptT) return false;
+  switch (b.L) {
+    case 2: err = wpt1_l<2>(b, a, s, fwd); return true;
+    case 4: err = wpt1_l<4>(b, a, s, fwd); return true;
+    case 8: err = wpt1_l<8>(b, a, s, fwd); return true;
+    case 16: err = wpt1_l<16>(b, a, s, fwd); return true;
     default: return false;
   }
 }

@@ -1,0 +1,260 @@
+// wpt1_kernels.hpp — Wavelet Packet Transform tile kernels for contiguous
+// packets (C = 1, stride 1, 16-B aligned rows) with compile-time geometry
+// (tap count L, tile T, fused levels K).
+//
+// Reference: WaveletPacketTransform.forward (WaveletPacketTransform.java:73-124)
+// transforms every packet of a level with Wavelet.forward (wrap inside the
+// packet), output per packet [a | d], packet p of level l splitting into
+// packets 2p (a) and 2p+1 (d) of level l+1; reverse (:141-191) undoes it
+// level by level.  Math and summation order are those of Wavelet.forward /
+// Wavelet.reverse (Wavelet.java:236-303), as in fwt_kernels.hpp.
+//
+// A block owns T consecutive samples (tile t) of one row (a packet of size h
+// at the pass start) and runs K levels in LDS; only the last level touches
+// HBM, so one pass reads and writes the array once.
+//  forward: level-0 window [tT, tT + T + (L-2)(2^K-1)) mod h; level l holds
+//           2^l sub-windows (one per packet) of m_l = T/2^l + (L-2)(2^(K-l)-1)
+//           samples; periodicity of the row carries over to every packet.
+//  reverse: level-l windows [tT/2^l - c_l, (t+1)T/2^l) of all 2^l packets
+//           (c_l as in fwt1_kernels.hpp); level 0 = the T outputs.
+// Levels run in place: every lane computes its pairs into registers, a
+// barrier, then writes (two LDS-only barriers per level).
+#pragma once
+#include "fwt1_kernels.hpp"
+
+namespace jwv {
+
+// ---------------------------------------------------------------- forward
+template <int L, int T, int K>
+struct Wpt1FwdGeo {
+  static constexpr int m(int l) { return (T >> l) + (L - 2) * ((1 << (K - l)) - 1); }
+  static constexpr int lds_doubles() { return m(0) + 2; }
+  static_assert((L & 1) == 0 && ((T >> K) & 1) == 0, "even windows");
+};
+
+template <int L, int NT, int T, int K, bool FMA, int l>
+struct Wpt1FwdLevel {
+  // lds: 2^(l-1) input sub-windows of m(l-1) samples (stride m(l-1)).
+  __device__ __forceinline__ static void run(const FwdTaps<L>& tp, double* lds, int h, int t,
+                                             double* __restrict__ y) {
+    using G = Wpt1FwdGeo<L, T, K>;
+    constexpr int mi = G::m(l - 1), mo = G::m(l);
+    constexpr int NC = (1 << (l - 1)) * (mo / 2);  // pair couples (2 adjacent pairs)
+    constexpr int R = (NC + NT - 1) / NT;
+    const int tid = opaque_tid();  // per-level: keeps address math out of the prologue
+    double2 ra[R], rd[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int q = tid + r * NT;
+      if ((r + 1) * NT <= NC || q < NC) {
+        const int s = q / (mo / 2), i = 2 * (q % (mo / 2));  // sub-window, first pair
+        const double* in = lds + s * mi + 2 * i;
+        double x[L + 2];
+#pragma unroll
+        for (int j = 0; j < L + 2; j += 2) {
+          const double2 v = *reinterpret_cast<const double2*>(in + j);
+          x[j] = v.x;
+          x[j + 1] = v.y;
+        }
+        double a0, d0, a1, d1;
+        fwd_pair<L, FMA>(tp, [&](int j) { return x[j]; }, a0, d0);
+        fwd_pair<L, FMA>(tp, [&](int j) { return x[j + 2]; }, a1, d1);
+        // slot boundary: results exist here and later slots' LDS reads stay
+        // below, so the compiler cannot hoist all slots' windows at once
+        // (L = 16: ~190 VGPRs, 2 waves/SIMD -> ~80 VGPRs)
+        asm volatile("" : "+v"(a0), "+v"(a1), "+v"(d0), "+v"(d1) :: "memory");
+        if constexpr (l == K) {
+          // packets 2s (a) and 2s+1 (d) of size h/2^K; own range t*T/2^K + i
+          const int hp = h >> K;
+          double* pa = y + (int64_t)(2 * s) * hp + t * (T >> K) + i;
+          *reinterpret_cast<double2*>(pa) = make_double2(a0, a1);
+          *reinterpret_cast<double2*>(pa + hp) = make_double2(d0, d1);
+        } else {
+          ra[r] = make_double2(a0, a1);
+          rd[r] = make_double2(d0, d1);
+        }
+      }
+    }
+    if constexpr (l < K) {
+      lds_barrier();
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int q = tid + r * NT;
+        if ((r + 1) * NT <= NC || q < NC) {
+          const int s = q / (mo / 2), i = 2 * (q % (mo / 2));
+          *reinterpret_cast<double2*>(lds + (2 * s) * mo + i) = ra[r];
+          *reinterpret_cast<double2*>(lds + (2 * s + 1) * mo + i) = rd[r];
+        }
+      }
+      lds_barrier();
+      Wpt1FwdLevel<L, NT, T, K, FMA, l + 1>::run(tp, lds, h, t, y);
+    }
+  }
+};
+
+// Grid: rows * (h / T) blocks; row o = packet o of the pass input (view sv,
+// packets addressed through view_base); output rows likewise (view dv).
+template <int L, int NT, int T, int K, bool FMA>
+__global__ __launch_bounds__(NT) void wpt_fwd_tile1(const double* __restrict__ src, AxisView sv,
+                                                    double* __restrict__ dst, AxisView dv, int h,
+                                                    FwdTaps<L> tp) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  using G = Wpt1FwdGeo<L, T, K>;
+  constexpr int M0 = G::m(0);
+  const int ntile = h / T;
+  const int nblk = gridDim.x;
+  int b = blockIdx.x;
+  if ((nblk & 7) == 0) b = (b & 7) * (nblk >> 3) + (b >> 3);
+  const int t = b % ntile;
+  const int64_t o = b / ntile;
+  const double* s = src + view_base(sv, o);
+  const int msk = h - 1, base = t * T;
+  load_window<1, NT, (M0 + NT - 1) / NT>(lds, s, M0, true, 0, 1,
+                                          [&](int e) { return (int64_t)((base + e) & msk); });
+  dma_fence_barrier();
+  Wpt1FwdLevel<L, NT, T, K, FMA, 1>::run(tp, lds, h, t, dst + view_base(dv, o));
+}
+
+// ---------------------------------------------------------------- reverse
+template <int L, int T, int K>
+struct Wpt1RevGeo {
+  using R = Rev1Geo<L, T, K>;
+  static constexpr int len(int l) { return R::len(l); }
+  static constexpr int c(int l) { return R::c(l); }
+  // + 4: the odd-window couple tail reads up to two samples past a window
+  static constexpr int lds_doubles() { return (1 << K) * len(K) + 4; }
+};
+
+template <int L, int NT, int T, int K, bool FMA, int l>
+struct Wpt1RevLevel {
+  // lds: 2^l packet windows of len(l) (stride len(l)); produces 2^(l-1)
+  // windows of len(l-1) (level 1: the T outputs, to y).  Each lane computes
+  // two adjacent pairs (ml, ml+1) from Q+2 registers per operand read with
+  // (Q+2)/2 conflict-free 16-B LDS reads (lane stride 16 B).
+  // Array-head pairs (global pair index < Q-1, Wavelet.java:284-296 order)
+  // occur only in the first tiles: there, lanes tid < 2^(l-1)(Q-1) compute one
+  // head pair each, and the couples skip storing them (one copy of the head
+  // code per level instead of one per unrolled slot).
+  __device__ __forceinline__ static void run(const RevTaps<L>& tp, double* lds, int t,
+                                             double* __restrict__ y) {
+    using G = Wpt1RevGeo<L, T, K>;
+    constexpr int Q = L / 2;
+    constexpr int li_ = G::len(l), lo_ = G::len(l - 1);
+    constexpr int NW = 1 << (l - 1);                // output windows
+    constexpr int NPW = lo_ / 2;                    // pairs per output window
+    constexpr int NCW = (NPW + 1) / 2;              // couples per output window
+    constexpr int NC = NW * NCW;                    // couples of the level
+    constexpr int off = G::c(l) - G::c(l - 1) / 2;  // local index of a[pair 0]
+    // couple k reads a[off + 2k - (Q-1) .. off + 2k + 1] from an even start
+    constexpr int sh = (off - (Q - 1)) & 1;         // 1: start one lower
+    constexpr int NR = (Q + 3) & ~1;                // registers per operand (even, >= Q+2)
+    constexpr int R = (NC + NT - 1) / NT;
+    static_assert(NW * (Q - 1) <= NT, "one head pair per lane");
+    const int tid = opaque_tid();  // per-level: keeps address math out of the prologue
+    const int pbase = t * (T >> l) - G::c(l - 1) / 2;  // global index of pair 0
+    const bool head_tile = pbase < Q - 1;              // block-uniform
+    double4 rx[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int k = tid + r * NT;
+      if ((r + 1) * NT <= NC || k < NC) {
+        const int s = k / NCW, ml = 2 * (k % NCW);
+        const double* ab = lds + (2 * s) * li_;
+        const double* db = ab + li_;
+        const int st = off + ml - (Q - 1) - sh;  // even
+        double av[NR], dv[NR];
+#pragma unroll
+        for (int j = 0; j < NR; j += 2) {
+          const double2 u = *reinterpret_cast<const double2*>(ab + st + j);
+          const double2 w = *reinterpret_cast<const double2*>(db + st + j);
+          av[j] = u.x; av[j + 1] = u.y;
+          dv[j] = w.x; dv[j + 1] = w.y;
+        }
+        // pair ml: a[li - q] = av[(Q-1) + sh - q]; pair ml+1: one further
+        double x0e, x0o, x1e, x1o;
+        rev_pair<L, FMA>(tp, av + (Q - 1) + sh, dv + (Q - 1) + sh, 1, x0e, x0o);
+        rev_pair<L, FMA>(tp, av + Q + sh, dv + Q + sh, 1, x1e, x1o);
+        asm volatile("" : "+v"(x0e), "+v"(x0o), "+v"(x1e), "+v"(x1o) :: "memory");  // slot boundary
+        const int mg = pbase + ml;
+        const bool w0 = !(head_tile && mg >= 0 && mg < Q - 1);
+        const bool w1 = ((NPW % 2 == 0) || ml + 1 < NPW) &&
+                        !(head_tile && mg + 1 >= 0 && mg + 1 < Q - 1);
+        if constexpr (l == 1) {
+          double* yo = y + (int64_t)t * T + 2 * ml;
+          if (w0) *reinterpret_cast<double2*>(yo) = make_double2(x0e, x0o);
+          if (w1) *reinterpret_cast<double2*>(yo + 2) = make_double2(x1e, x1o);
+        } else {
+          rx[r] = make_double4(x0e, x0o, x1e, x1o);  // store flags recomputed below
+        }
+      }
+    }
+    // head pairs: lane -> (window hs, global pair hm)
+    int hs = -1, hml = 0;
+    double hxe = 0.0, hxo = 0.0;
+    if (head_tile && tid < NW * (Q - 1)) {
+      const int s = tid / (Q - 1), m = tid % (Q - 1), ml = m - pbase;
+      if (ml >= 0 && ml < NPW) {
+        const double* ab = lds + (2 * s) * li_;
+        const double* db = ab + li_;
+        const int li = off + ml;
+        rev_pair_head<L, FMA>(
+            tp, m, [=](int q) { return ab[li - q]; }, [=](int q) { return db[li - q]; }, hxe, hxo);
+        hs = s;
+        hml = ml;
+      }
+    }
+    if constexpr (l == 1) {
+      if (hs >= 0) *reinterpret_cast<double2*>(y + (int64_t)t * T + 2 * hml) = make_double2(hxe, hxo);
+    } else {
+      lds_barrier();
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int k = tid + r * NT;
+        if ((r + 1) * NT <= NC || k < NC) {
+          const int s = k / NCW, ml = 2 * (k % NCW);
+          const int mg = pbase + ml;
+          const bool w0 = !(head_tile && mg >= 0 && mg < Q - 1);
+          const bool w1 = ((NPW % 2 == 0) || ml + 1 < NPW) &&
+                          !(head_tile && mg + 1 >= 0 && mg + 1 < Q - 1);
+          double* ob = lds + s * lo_ + 2 * ml;
+          if (w0) *reinterpret_cast<double2*>(ob) = make_double2(rx[r].x, rx[r].y);
+          if (w1) *reinterpret_cast<double2*>(ob + 2) = make_double2(rx[r].z, rx[r].w);
+        }
+      }
+      if (hs >= 0) *reinterpret_cast<double2*>(lds + hs * lo_ + 2 * hml) = make_double2(hxe, hxo);
+      lds_barrier();
+      Wpt1RevLevel<L, NT, T, K, FMA, l - 1>::run(tp, lds, t, y);
+    }
+  }
+};
+
+// Grid: rows * (h / T) blocks; h = output packet size of the pass; input
+// row o holds 2^K packets of h/2^K (view sv), output row o (view dv).
+template <int L, int NT, int T, int K, bool FMA>
+__global__ __launch_bounds__(NT) void wpt_rev_tile1(const double* __restrict__ src, AxisView sv,
+                                                    double* __restrict__ dst, AxisView dv, int h,
+                                                    RevTaps<L> tp) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  using G = Wpt1RevGeo<L, T, K>;
+  constexpr int LK = G::len(K);
+  constexpr int NW = 1 << K;
+  const int ntile = h / T;
+  const int nblk = gridDim.x;
+  int b = blockIdx.x;
+  if ((nblk & 7) == 0) b = (b & 7) * (nblk >> 3) + (b >> 3);
+  const int t = b % ntile;
+  const int64_t o = b / ntile;
+  const double* s = src + view_base(sv, o);
+  const int hp = h >> K, pm = hp - 1;
+  const int BK = t * (T >> K) - G::c(K);
+  // all 2^K packet windows in one burst: window w -> lds[w * LK ..)
+  load_window<1, NT, (NW * LK + NT - 1) / NT>(
+      lds, s, NW * LK, true, 0, 1, [&](int e) {
+        const int w = e / LK, k = e - w * LK;
+        return (int64_t)w * hp + ((BK + k) & pm);
+      });
+  dma_fence_barrier();
+  Wpt1RevLevel<L, NT, T, K, FMA, K>::run(tp, lds, t, dst + view_base(dv, o));
+}
+
+}  // namespace jwv
