@@ -151,6 +151,24 @@ int jwv_fwt3d_fwd_f64_dev(const double* x, double* y, int64_t p, int64_t q, int6
 int jwv_fwt3d_rev_f64_dev(const double* y, double* x, int64_t p, int64_t q, int64_t r,
                           int lvl_p, int lvl_q, int lvl_r, const jwv_taps* t, jwv_ctx* ctx);
 
+/* ---- CompressorMagnitude / denoise ---------------------------------------------
+ * CompressorMagnitude(threshold).compress(double[])
+ * (compressions/CompressorMagnitude.java:73-84, Compressor.java:96-110):
+ * y[i] = |x[i]| >= m * threshold ? x[i] : 0 with m = sum|x| / n.  A threshold
+ * <= 0 becomes 1.0 (Compressor.java:66-80).  m is summed as a fixed tree on
+ * the device (deterministic; not the JVM's left-to-right order, so it can
+ * differ in the last bits).  magnitude: optional host pointer for m.
+ * jwv_fwt_denoise_*: forward(level) -> compress -> reverse(level) without
+ * leaving the device (the Transform + Compressor denoising sequence). */
+int jwv_compress_magnitude_f64(const double* x, double* y, int64_t n, double threshold,
+                               double* magnitude, jwv_ctx* ctx);
+int jwv_compress_magnitude_f64_dev(const double* x, double* y, int64_t n, double threshold,
+                                   double* magnitude, jwv_ctx* ctx);
+int jwv_fwt_denoise_f64(const double* x, double* y, int64_t n, int level, double threshold,
+                        const jwv_taps* t, jwv_ctx* ctx);
+int jwv_fwt_denoise_f64_dev(const double* x, double* y, int64_t n, int level, double threshold,
+                            const jwv_taps* t, jwv_ctx* ctx);
+
 /* ---- one axis of a block -------------------------------------------------------
  * The per-dimension pass inside BasicTransform's 2-D/3-D loops
  * (BasicTransform.java:369-395 rows / columns, :520-558 lines along i): the

@@ -80,6 +80,10 @@ for _n in ("wpt3d_fwd", "wpt3d_rev"):
     _SIGS["jwv_%s_f64" % _n] = [_dp, _dp, _i64, _i64, _i64, _int, _int, _int, _TP, _CTX]
 for _n in ("fwt_axis_fwd", "fwt_axis_rev", "wpt_axis_fwd", "wpt_axis_rev"):
     _SIGS["jwv_%s_f64_dev" % _n] = [_dp, _dp, _i64, _i64, _i64, _int, _TP, _CTX]
+for _s in ("", "_dev"):
+    _SIGS["jwv_compress_magnitude_f64%s" % _s] = [_dp, _dp, _i64, ctypes.c_double,
+                                                  ctypes.POINTER(ctypes.c_double), _CTX]
+    _SIGS["jwv_fwt_denoise_f64%s" % _s] = [_dp, _dp, _i64, _int, ctypes.c_double, _TP, _CTX]
 for _n in ("modwt_fwd", "modwt_inv"):
     for _s in ("", "_dev"):
         _SIGS["jwv_%s_f64%s" % (_n, _s)] = [_dp, _dp, _i64, _int, _TP, _CTX]

@@ -51,6 +51,7 @@ struct jwv_ctx {
   DevBuf ws[2];  // small ping-pong scratch (level approximations)
   DevBuf big;    // full-size intermediate between 2-D/3-D axes
   DevBuf big2;   // full-size intermediate between multi-pass WPT passes
+  DevBuf red;    // reduction scratch (CompressorMagnitude)
   DevBuf hin, hout;  // staging for the host-pointer entry points
   // profiling: hipEvent pairs around every kernel launch on the launch stream
   bool prof = false;
@@ -819,7 +820,7 @@ int jwv_ctx_destroy(jwv_ctx* c) {
   if (!c) return JWV_OK;
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
-  for (DevBuf* b : {&c->ws[0], &c->ws[1], &c->big, &c->big2, &c->hin, &c->hout})
+  for (DevBuf* b : {&c->ws[0], &c->ws[1], &c->big, &c->big2, &c->red, &c->hin, &c->hout})
     if (b->p) hipFree(b->p);
   for (auto& r : c->recs) { hipEventDestroy(r.e0); hipEventDestroy(r.e1); }
   for (auto e : c->ev_pool) hipEventDestroy(e);
@@ -906,7 +907,7 @@ int jwv_ctx_profile_read(jwv_ctx* c, jwv_kernel_stat* out, int max_out, int* n_o
 int jwv_ctx_trim(jwv_ctx* c) {
   return guarded(c, [&] {
     hipchk(hipStreamSynchronize(c->stream), "sync");
-    for (DevBuf* b : {&c->ws[0], &c->ws[1], &c->big, &c->big2, &c->hin, &c->hout}) {
+    for (DevBuf* b : {&c->ws[0], &c->ws[1], &c->big, &c->big2, &c->red, &c->hin, &c->hout}) {
       if (b->p) hipchk(hipFree(b->p), "free");
       b->p = nullptr;
       b->n = 0;
@@ -1083,6 +1084,86 @@ JWV_3D(jwv_fwt3d_fwd_f64_dev, Kind::FWT, true, true)
 JWV_3D(jwv_fwt3d_rev_f64_dev, Kind::FWT, false, true)
 JWV_3D(jwv_wpt3d_fwd_f64, Kind::WPT, true, false)
 JWV_3D(jwv_wpt3d_rev_f64, Kind::WPT, false, false)
+
+// ---- CompressorMagnitude / denoise ---------------------------------------------------
+namespace {
+// Compressor(double threshold) (compressions/Compressor.java:66-80): a
+// threshold <= 0 is reported and replaced by the default 1.0.
+double compressor_threshold(double t) { return t > 0.0 ? t : 1.0; }
+
+// y = CompressorMagnitude.compress(c) (CompressorMagnitude.java:73-84) on the
+// device; the magnitude is copied to *mag (host) when mag != NULL (syncs).
+void body_compress(jwv_ctx* c, const double* x, double* y, int64_t n, double threshold,
+                   double* mag) {
+  if (n == 0) return;
+  const int np = jwv::compress_partials(n);
+  double* scratch = grow(c, c->red, (size_t)np + 2);
+  hipchk(jwv::launch_compress_magnitude(x, y, n, compressor_threshold(threshold), scratch,
+                                        c->stream),
+         "compress_magnitude");
+  if (mag) {
+    hipchk(hipMemcpyAsync(mag, scratch + np + 1, sizeof(double), hipMemcpyDeviceToHost, c->stream),
+           "D2H");
+    hipchk(hipStreamSynchronize(c->stream), "sync");
+  }
+}
+
+// forward (level) -> CompressorMagnitude(threshold) -> reverse (level), all on
+// the device: the usual denoising use of Transform + Compressor.
+void body_denoise(jwv_ctx* c, const Bank& b, const double* x, double* y, int64_t n, int level,
+                  double threshold) {
+  if (n == 0) return;
+  double* coef = grow(c, c->big, (size_t)n);
+  body_1d(c, Kind::FWT, true, b, x, coef, 1, n, n, level);
+  body_compress(c, coef, coef, n, threshold, nullptr);
+  body_1d(c, Kind::FWT, false, b, coef, y, 1, n, n, level);
+}
+}  // namespace
+
+int jwv_compress_magnitude_f64(const double* x, double* y, int64_t n, double threshold,
+                               double* magnitude, jwv_ctx* c) {
+  return guarded(c, [&] {
+    if (n < 0) throw Fail{JWV_ERR_BAD_CALL, "n < 0"};
+    if (n == 0) return;
+    check_ptrs(x, y);
+    staged(c, x, (size_t)n, y, (size_t)n,
+           [&](const double* dx, double* dy) { body_compress(c, dx, dy, n, threshold, nullptr); });
+    if (magnitude) {
+      const int np = jwv::compress_partials(n);
+      hipchk(hipMemcpy(magnitude, c->red.p + np + 1, sizeof(double), hipMemcpyDeviceToHost), "D2H");
+    }
+  });
+}
+int jwv_compress_magnitude_f64_dev(const double* x, double* y, int64_t n, double threshold,
+                                   double* magnitude, jwv_ctx* c) {
+  return guarded(c, [&] {
+    if (n < 0) throw Fail{JWV_ERR_BAD_CALL, "n < 0"};
+    if (n == 0) return;
+    need_device_ptrs(x, y);
+    body_compress(c, x, y, n, threshold, magnitude);
+  });
+}
+int jwv_fwt_denoise_f64(const double* x, double* y, int64_t n, int level, double threshold,
+                        const jwv_taps* t, jwv_ctx* c) {
+  return guarded(c, [&] {
+    const Bank b = make_bank(t);
+    check_1d(Kind::FWT, true, n, level);
+    if (n == 0) return;
+    check_ptrs(x, y);
+    staged(c, x, (size_t)n, y, (size_t)n,
+           [&](const double* dx, double* dy) { body_denoise(c, b, dx, dy, n, level, threshold); });
+  });
+}
+int jwv_fwt_denoise_f64_dev(const double* x, double* y, int64_t n, int level, double threshold,
+                            const jwv_taps* t, jwv_ctx* c) {
+  return guarded(c, [&] {
+    const Bank b = make_bank(t);
+    check_1d(Kind::FWT, true, n, level);
+    if (n == 0) return;
+    need_device_ptrs(x, y);
+    body_denoise(c, b, x, y, n, level, threshold);
+  });
+}
 
 // ---- MODWT -------------------------------------------------------------------------
 int jwv_modwt_filters(const jwv_taps* t, double* g, double* h) {

@@ -69,7 +69,7 @@ struct Geo {
   static constexpr int kFwtT8 = 512, kFwtK8 = 3;
   static constexpr int kWptT1 = 8192, kWptK1 = 6;
   static constexpr int kWptT8 = 512, kWptK8 = 3;
-  static constexpr int kModT = 4096, kModS = 2048;
+  static constexpr int kModT = 4096, kModTInv = 1024, kModS = 2048;
   static int res_cap(int C) { return C == 1 ? kResCap1 : kResCap8; }
   // tile of the C = 1 FWT passes: 4096 (default) or 2048, env JWV_FWD_T / JWV_REV_T;
   // reverse detail prefetch-all: env JWV_REV_PREF=1
@@ -109,6 +109,13 @@ hipError_t launch_modwt_inv(const Bank& modwt_gh, bool fma, bool tiled, const Mo
                             hipStream_t);
 hipError_t launch_copy_axis(const double* src, AxisView sv, double* dst, AxisView dv,
                             int64_t nouter, int len, int inner, hipStream_t);
+
+// CompressorMagnitude (launch_compress.hip): y = c with |c| < mean|c| *
+// threshold zeroed; scratch holds compress_partials(n) + 2 doubles (the
+// magnitude lands in scratch[compress_partials(n) + 1]).
+int compress_partials(int64_t n);
+hipError_t launch_compress_magnitude(const double* c, double* y, int64_t n, double threshold,
+                                     double* scratch, hipStream_t s);
 
 // Per-mode entry points implemented by launch_{fwt,wpt,modwt}.hip compiled
 // twice (JWV_FMA=0 / 1).

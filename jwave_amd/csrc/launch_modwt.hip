@@ -18,6 +18,7 @@ namespace {
 constexpr bool kFMA = JWV_FMA != 0;
 constexpr int NT = 256;
 constexpr int T = Geo::kModT;
+constexpr int TI = Geo::kModTInv;  // inverse: two windows in LDS, smaller tile
 constexpr int SMAX = Geo::kModS;
 
 // Bank.lo / Bank.hi carry the MODWT g / h filters here (see capi.cpp).
@@ -65,11 +66,11 @@ template <int L>
 hipError_t inv_go(const Bank& b, bool tiled, const ModwtArgs& a, hipStream_t s) {
   const auto tp = mtaps<L>(b);
   if (tiled) {
-    auto k = modwt_inv_tile<L, NT, T, SMAX, kFMA>;
+    auto k = modwt_inv_tile<L, NT, TI, SMAX, kFMA>;
     const int R = (b.L - 1) * ((1 << a.j1) - (1 << (a.j0 - 1)));
-    const size_t lds = (size_t)2 * (T + R) * sizeof(double);
+    const size_t lds = (size_t)2 * (TI + R) * sizeof(double);
     if (hipError_t e = prep(k, lds)) return e;
-    const dim3 grid((unsigned)((a.N + T - 1) / T));
+    const dim3 grid((unsigned)((a.N + TI - 1) / TI));
     hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.coef, a.ldw, a.vout, a.N, a.j0, a.j1,
                        tp);
   } else {

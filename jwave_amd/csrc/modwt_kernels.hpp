@@ -126,7 +126,9 @@ __global__ __launch_bounds__(256) void modwt_fwd_level(const double* __restrict_
 }
 
 // Inverse, tiled: levels j1 down to j0.  vsrc = V_{j1}; W_j at coef+(j-1)*ldw;
-// output V_{j0-1} -> dst.  LDS: 2 * (T + R) doubles.
+// output V_{j0-1} -> dst.  LDS: 2 * (T + R) doubles.  The W window of the
+// next level is loaded into registers while the current level computes, so
+// each block pays one exposed HBM latency instead of one per level.
 template <int L, int NT, int T, int SMAX, bool FMA>
 __global__ __launch_bounds__(NT) void modwt_inv_tile(const double* __restrict__ vsrc,
                                                      const double* __restrict__ coef, int64_t ldw,
@@ -140,16 +142,30 @@ __global__ __launch_bounds__(NT) void modwt_inv_tile(const double* __restrict__ 
   double* wb = lds + (T + R);
   const int64_t t0 = (int64_t)blockIdx.x * T;
   const int tid = threadIdx.x;
+  // W window of level j (length T + Rj) -> registers (all loads in flight)
+  double pw[MAXP];
+  auto fetch_w = [&](int j, int W) {
+    const double* wrow = coef + (int64_t)(j - 1) * ldw;
+#pragma unroll
+    for (int r = 0; r < MAXP; ++r) {
+      const int q = tid + r * NT;
+      pw[r] = q < W ? wrow[wrap_mod(t0 + q, N)] : 0.0;
+    }
+  };
   load_window<1, NT, MAXP>(vb, vsrc, T + R, false, 0, 1,
                            [&](int e) { return wrap_mod(t0 + e, N); });
+  fetch_w(j1, T + R);
   int Rj = R;
   for (int j = j1; j >= j0; --j) {
     const int st = 1 << (j - 1);
     const int Rn = Rj - (nL - 1) * st;
-    const double* wrow = coef + (int64_t)(j - 1) * ldw;
-    load_window<1, NT, MAXP>(wb, wrow, T + Rj, false, 0, 1,
-                             [&](int e) { return wrap_mod(t0 + e, N); });
+#pragma unroll
+    for (int r = 0; r < MAXP; ++r) {
+      const int q = tid + r * NT;
+      if (q < T + Rj) wb[q] = pw[r];
+    }
     lds_barrier();
+    if (j > j0) fetch_w(j - 1, T + Rn);  // next level's W, in flight during this level
     const int nout = T + Rn;
     double vv[MAXP];
 #pragma unroll
@@ -178,7 +194,7 @@ __global__ __launch_bounds__(NT) void modwt_inv_tile(const double* __restrict__ 
         const int p = tid + r * NT;
         if (p < nout) vb[p] = vv[r];
       }
-      lds_barrier();
+      // (the barrier at the top of the next level orders these writes)
     }
     Rj = Rn;
   }

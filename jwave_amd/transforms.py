@@ -146,6 +146,12 @@ def _is_torch(x):
     return type(x).__module__.startswith("torch")
 
 
+def _is_complex(x):
+    if _is_torch(x):
+        return x.is_complex()
+    return np.iscomplexobj(x)
+
+
 def _prep(x, ctx):
     """-> (ptr, keepalive, is_device, like) for an input array."""
     if _is_torch(x):
@@ -261,6 +267,48 @@ def modwt_inverse(coeffs, wavelet, ctx=None):
                 (n, int(J), _TapsHolder.of(wavelet)))
 
 
+def compress_magnitude(x, threshold=1.0, ctx=None):
+    """CompressorMagnitude(threshold).compress(x) on the GPU -> (y, magnitude)
+    (compressions/CompressorMagnitude.java:73-84; DESIGN.md: the magnitude sum
+    order differs from the JVM's, so it may differ in the last bits)."""
+    ctx = ctx or default_context()
+    n = int(x.shape[0])
+    mag = ctypes.c_double(0.0)
+    y = _run("jwv_compress_magnitude_f64", "jwv_compress_magnitude_f64_dev", ctx, x, (n,),
+             (n, float(threshold), ctypes.byref(mag)))
+    return y, mag.value
+
+
+def fwt_denoise(x, wavelet, level, threshold=1.0, ctx=None):
+    """forward(level) -> CompressorMagnitude(threshold) -> reverse(level), on
+    the device (the Transform + Compressor denoising sequence)."""
+    n = int(x.shape[0])
+    return _run("jwv_fwt_denoise_f64", "jwv_fwt_denoise_f64_dev", ctx, x, (n,),
+                (n, int(level), float(threshold), _TapsHolder.of(wavelet)))
+
+
+class CompressorMagnitude:
+    """jwave.compressions.CompressorMagnitude (CompressorMagnitude.java:35-136),
+    1-D on the GPU."""
+
+    def __init__(self, threshold=1.0, ctx=None):
+        if threshold <= 0.0:  # Compressor.java:66-80: reported, default used
+            threshold = 1.0
+        self._threshold = float(threshold)
+        self._magnitude = 0.0
+        self._ctx = ctx
+
+    def compress(self, arr):
+        y, self._magnitude = compress_magnitude(arr, self._threshold, self._ctx)
+        return y
+
+    @staticmethod
+    def calcCompressionRate(arr):  # noqa: N802 — Compressor.java:152-166
+        a = np.asarray(arr.cpu() if _is_torch(arr) else arr)
+        zeros = int(np.count_nonzero(a == 0.0))
+        return zeros / a.shape[0] * 100.0 if zeros else 0.0
+
+
 def modwt_filters(wavelet):
     g = np.empty(wavelet.mother_wavelength)
     h = np.empty(wavelet.mother_wavelength)
@@ -294,6 +342,8 @@ class BasicTransform:
 
     # -- overload dispatch --------------------------------------------------
     def forward(self, a, *levels):
+        if _is_complex(a):
+            return self._complex(a, True)
         nd = len(np.shape(a)) if not _is_torch(a) else a.dim()
         if nd == 1:
             return self.forward_1d(a, *levels)
@@ -304,6 +354,8 @@ class BasicTransform:
         raise JWaveFailure("unsupported array rank %d" % nd)
 
     def reverse(self, a, *levels):
+        if _is_complex(a):
+            return self._complex(a, False)
         nd = len(np.shape(a)) if not _is_torch(a) else a.dim()
         if nd == 1:
             return self.reverse_1d(a, *levels)
@@ -312,6 +364,22 @@ class BasicTransform:
         if nd == 3:
             return self.reverse_3d(a, *levels)
         raise JWaveFailure("unsupported array rank %d" % nd)
+
+    # -- Complex[]: BasicTransform.java:257-322 -----------------------------
+    def _complex(self, a, fwd):
+        """forward/reverse(Complex[]): real and imaginary parts interleaved
+        {r0, i0, r1, i1, ..} into one real array of 2n, transformed at full
+        depth (the single-argument forward/reverse), then split again."""
+        if _is_torch(a):
+            import torch
+            bulk = torch.view_as_real(a.contiguous()).reshape(-1).to(torch.float64).contiguous()
+            out = self.forward_1d(bulk) if fwd else self.reverse_1d(bulk)
+            return torch.view_as_complex(out.reshape(-1, 2).contiguous())
+        z = np.asarray(a, dtype=np.complex128)
+        bulk = np.empty(2 * z.shape[0])
+        bulk[0::2], bulk[1::2] = z.real, z.imag
+        out = np.asarray(self.forward_1d(bulk) if fwd else self.reverse_1d(bulk))
+        return out[0::2] + 1j * out[1::2]
 
     # -- 2-D: BasicTransform.java:336-474 ----------------------------------
     def forward_2d(self, m, lvl_m=None, lvl_n=None):
@@ -530,6 +598,71 @@ class MODWTTransform(WaveletTransform):
 
     def _check_1d(self, n, level, fwd):
         pass
+
+
+def decompose_number(number, block_size=None):
+    """MathToolKit.decompose(int) (tools/MathToolKit.java:57-80): the powers
+    of the ancient Egyptian decomposition, largest first (42 -> [5, 3, 1]);
+    with block_size (:97-138): full blocks of block_size first (entries are
+    the block size itself, as in the reference), then the decomposition of
+    the rest."""
+    number = int(number)
+    if block_size is not None:
+        block_size = int(block_size)
+        if not is_binary(block_size):
+            raise JWaveFailure("given block size is not 2^p|p={1,2,3,4,..}. "
+                               "block size shold be e. g.: 4, 8, 16, 32, ..")
+        if number < block_size:
+            raise JWaveFailure("Given blockSize is greater than the given number "
+                               "to be split by it")
+        nb = number // block_size
+        rest = number - nb * block_size
+        return [block_size] * nb + decompose_number(rest)
+    if number < 1:
+        raise JWaveFailure("the supported number for decomposition is smaller than one")
+    out = []
+    cur = number
+    while cur >= 1:
+        p = cur.bit_length() - 1
+        out.append(p)
+        cur -= 1 << p
+    return out
+
+
+class AncientEgyptianDecomposition(BasicTransform):
+    """jwave.transforms.AncientEgyptianDecomposition (AncientEgyptianDecomposition.java:47-184):
+    an array of arbitrary length is split into sub-arrays of the powers of
+    two of its length (largest first, MathToolKit.decompose); each goes
+    through the wrapped transform's full-depth forward / reverse (one native
+    call per sub-array, on the GPU) and lands at its original offset."""
+
+    def __init__(self, basic_transform, initial_wavelet_space_size=0):
+        super().__init__(basic_transform.getWavelet() if basic_transform._wavelet else None,
+                         basic_transform._ctx)
+        self._basic = basic_transform
+        self._name = "Ancient Egyptian Decomposition"
+
+    def _run(self, a, fwd):
+        n = a.shape[0]
+        if _is_torch(a):
+            import torch
+            out = torch.empty_like(a)
+        else:
+            a = np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+            out = np.empty_like(a)
+        off = 0
+        for p in decompose_number(n):
+            m = 1 << p
+            sub = a[off:off + m]
+            out[off:off + m] = self._basic.forward_1d(sub) if fwd else self._basic.reverse_1d(sub)
+            off += m
+        return out
+
+    def forward_1d(self, arr, level=None):
+        return self._run(arr, True)
+
+    def reverse_1d(self, arr, level=None):
+        return self._run(arr, False)
 
 
 class Transform:

@@ -415,3 +415,17 @@ void orc_java_random_doubles(int64_t seed, double* out, int64_t n) {
     out[i] = (double)((a << 27) + b) * (1.0 / (double)(1ULL << 53));
   }
 }
+
+/* CompressorMagnitude.compress(double[]) (compressions/CompressorMagnitude.java:73-84)
+ * with Compressor.compress(arr, magnitude) (Compressor.java:96-110): the
+ * magnitude is the left-to-right sum of |x| divided by n; an entry survives
+ * iff |x| >= magnitude * threshold.  threshold <= 0 -> 1.0 (Compressor.java:66-80).
+ * Returns the magnitude. */
+double orc_compress_magnitude(const double* x, double* y, int64_t n, double threshold) {
+  if (threshold <= 0.0) threshold = 1.0;
+  double mag = 0.0;
+  for (int64_t i = 0; i < n; i++) mag += fabs(x[i]);
+  mag /= (double)n;
+  for (int64_t i = 0; i < n; i++) y[i] = fabs(x[i]) >= mag * threshold ? x[i] : 0.0;
+  return mag;
+}

@@ -160,3 +160,13 @@ def modwt_filters(wavelet):
     g = np.empty(L); h = np.empty(L); t = OracleTaps(wavelet)
     lib().orc_modwt_filters(t.ref(), _ptr(g), _ptr(h))
     return g, h
+
+
+def compress_magnitude(x, threshold):
+    """CompressorMagnitude(threshold).compress(x) -> (y, magnitude)."""
+    x = _f64(x); y = np.empty_like(x)
+    f = lib().orc_compress_magnitude
+    f.restype = ctypes.c_double
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_double]
+    mag = f(_ptr(x), _ptr(y), x.size, float(threshold))
+    return y, mag

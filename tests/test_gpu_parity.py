@@ -338,3 +338,90 @@ def test_axis_columns(ctx, kind, wname, R, cw, lev):
     x3 = torch.stack([xd, xd.flip(0)])
     y3 = T.transform_axis(x3, w, lev, 1, True, ctx, kind=kind)
     assert_exact(y3[0].cpu().numpy(), ref, "%s axis fwd 3d" % kind)
+
+
+@pytest.mark.parametrize("wname,n", [("Daubechies4", 1000), ("Haar1", 127), ("Symlet8", 70000),
+                                     ("Daubechies8", 1), ("Daubechies2", 3)])
+def test_ancient_egyptian_decomposition(ctx, wname, n):
+    """AncientEgyptianDecomposition over the native FWT
+    (AncientEgyptianDecomposition.java:97-184): every power-of-two sub-array
+    through the full-depth forward/reverse, bit-exact vs the oracle applied
+    to the same sub-arrays; numpy and device tensors."""
+    import torch
+    w = jw.by_class(wname)
+    aed = jw.AncientEgyptianDecomposition(jw.FastWaveletTransform(w, ctx))
+    x = rnd(n, seed=11)
+    ref = np.empty(n)
+    off = 0
+    for p in jw.decompose_number(n):
+        m = 1 << p
+        ref[off:off + m] = oracle.fwt_forward(w, x[off:off + m], p)
+        off += m
+    y = aed.forward(x)
+    assert_exact(y, ref, "aed fwd")
+    back = np.empty(n)
+    off = 0
+    for p in jw.decompose_number(n):
+        m = 1 << p
+        back[off:off + m] = oracle.fwt_reverse(w, ref[off:off + m], p)
+        off += m
+    assert_exact(aed.reverse(ref), back, "aed rev")
+    yd = aed.forward(torch.from_numpy(x).cuda())
+    assert_exact(yd.cpu().numpy(), ref, "aed fwd device")
+
+
+def test_complex_entry(ctx):
+    """BasicTransform.forward/reverse(Complex[]) (BasicTransform.java:257-322):
+    {re, im} interleaved into one real array of 2n at full depth."""
+    import torch
+    w = jw.by_class("Daubechies4")
+    fwt = jw.FastWaveletTransform(w, ctx)
+    n = 512
+    re, im = rnd(n, seed=3), rnd(n, seed=4)
+    z = re + 1j * im
+    bulk = np.empty(2 * n)
+    bulk[0::2], bulk[1::2] = re, im
+    ref = oracle.fwt_forward(w, bulk, 10)
+    y = fwt.forward(z)
+    assert_exact(np.asarray(y.real), ref[0::2], "complex fwd re")
+    assert_exact(np.asarray(y.imag), ref[1::2], "complex fwd im")
+    back = oracle.fwt_reverse(w, ref, 10)
+    zr = fwt.reverse(y)
+    assert_exact(np.asarray(zr.real), back[0::2], "complex rev re")
+    yd = fwt.forward(torch.from_numpy(z).cuda())
+    assert_exact(torch.view_as_real(yd).reshape(-1).cpu().numpy(), ref, "complex fwd device")
+
+
+@pytest.mark.parametrize("n,thr", [(1 << 12, 1.0), (1 << 20, 2.5), (1000, 0.0), (1, 1.0)])
+def test_compress_magnitude(ctx, n, thr):
+    """CompressorMagnitude.compress (CompressorMagnitude.java:73-84) on the
+    device vs the oracle's left-to-right restatement: magnitude within the
+    summation-order tolerance, output identical (no coefficient of this data
+    lies within n*eps of the cut)."""
+    w = jw.by_class("Daubechies4")
+    x = rnd(n, seed=5)
+    c = oracle.fwt_forward(w, x, int(n).bit_length() - 1) if n > 1 else x
+    ref, mag_ref = oracle.compress_magnitude(c, thr)
+    y, mag = jw.compress_magnitude(c, thr, ctx)
+    assert abs(mag - mag_ref) <= 1e-13 * max(1.0, abs(mag_ref)) * max(1.0, np.log2(n))
+    assert_exact(y, ref, "compress")
+    comp = jw.CompressorMagnitude(thr, ctx)
+    assert_exact(comp.compress(c), ref, "CompressorMagnitude")
+    assert comp.calcCompressionRate(ref) == pytest.approx(
+        100.0 * np.count_nonzero(ref == 0) / n if np.count_nonzero(ref == 0) else 0.0)
+
+
+@pytest.mark.parametrize("wname,n,lev", [("Daubechies4", 1 << 16, 16), ("Symlet8", 1 << 20, 12),
+                                         ("Haar1", 1 << 10, 10)])
+def test_fwt_denoise(ctx, wname, n, lev):
+    """forward -> CompressorMagnitude -> reverse fused on the device, vs the
+    same sequence on the oracle."""
+    import torch
+    w = jw.by_class(wname)
+    x = rnd(n, seed=9)
+    c = oracle.fwt_forward(w, x, lev)
+    cc, _ = oracle.compress_magnitude(c, 1.5)
+    ref = oracle.fwt_reverse(w, cc, lev)
+    assert_exact(jw.fwt_denoise(x, w, lev, 1.5, ctx), ref, "denoise")
+    yd = jw.fwt_denoise(torch.from_numpy(x).cuda(), w, lev, 1.5, ctx)
+    assert_exact(yd.cpu().numpy(), ref, "denoise device")
