@@ -400,7 +400,8 @@ def test_compress_magnitude(ctx, n, thr):
     lies within n*eps of the cut)."""
     w = jw.by_class("Daubechies4")
     x = rnd(n, seed=5)
-    c = oracle.fwt_forward(w, x, int(n).bit_length() - 1) if n > 1 else x
+    pow2 = n > 1 and (n & (n - 1)) == 0  # non-pow-2 sizes compress raw samples
+    c = oracle.fwt_forward(w, x, n.bit_length() - 1) if pow2 else x
     ref, mag_ref = oracle.compress_magnitude(c, thr)
     y, mag = jw.compress_magnitude(c, thr, ctx)
     assert abs(mag - mag_ref) <= 1e-13 * max(1.0, abs(mag_ref)) * max(1.0, np.log2(n))
