@@ -81,6 +81,18 @@ int jwv_ctx_set_stream(jwv_ctx* ctx, void* hip_stream);
 int jwv_ctx_reset_stream(jwv_ctx* ctx);
 void* jwv_ctx_get_stream(const jwv_ctx* ctx);
 int jwv_ctx_set_math(jwv_ctx* ctx, int mode);
+/* Pass plan for single long 1-D FWT signals (no reference counterpart; the
+ * results are bit-identical under every plan).  0 = the multi-launch plan.
+ * JWV_PLAN_REV_HEAD: the reverse's resident part and first tiled pass in one
+ * launch; JWV_PLAN_CHAIN_REV / _FWD: the whole reverse / forward in one launch.
+ * Default: JWV_PLAN_REV_HEAD (env JWV_PLAN overrides the default flags). */
+#define JWV_PLAN_CHAIN_REV 1
+#define JWV_PLAN_CHAIN_FWD 2
+#define JWV_PLAN_REV_HEAD 4
+int jwv_ctx_set_plan(jwv_ctx* ctx, int flags);
+/* Waits for the context's stream.  Also reports (JWV_ERR_DEVICE) a chained
+ * launch whose bounded in-kernel wait gave up since the last call (its results
+ * are then invalid; only possible if its grid was not co-resident). */
 int jwv_ctx_synchronize(jwv_ctx* ctx);
 /* Profiling: when enabled, every kernel launch is bracketed by a pair of
  * hipEvents recorded on the launch stream.  profile_read synchronises, sums the

@@ -21,6 +21,9 @@ JWV_ERR_DEVICE = 3
 JWV_ERR_BAD_CALL = 4
 JWV_MATH_EXACT = 0
 JWV_MATH_FMA = 1
+JWV_PLAN_CHAIN_REV = 1
+JWV_PLAN_CHAIN_FWD = 2
+JWV_PLAN_REV_HEAD = 4
 
 _dp = ctypes.c_void_p  # device or host double*
 _i64 = ctypes.c_int64
@@ -56,6 +59,7 @@ _SIGS = {
     "jwv_ctx_reset_stream": [_CTX],
     "jwv_ctx_get_stream": [_CTX],
     "jwv_ctx_set_math": [_CTX, _int],
+    "jwv_ctx_set_plan": [_CTX, _int],
     "jwv_ctx_synchronize": [_CTX],
     "jwv_ctx_trim": [_CTX],
     "jwv_ctx_profile_enable": [_CTX, _int],

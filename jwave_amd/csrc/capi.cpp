@@ -53,6 +53,11 @@ struct jwv_ctx {
   DevBuf big2;   // full-size intermediate between multi-pass WPT passes
   DevBuf red;    // reduction scratch (CompressorMagnitude)
   DevBuf hin, hout;  // staging for the host-pointer entry points
+  // single-launch FWT chains: [0, kWords) forward counters, [kWords, 2 kWords)
+  // reverse ticket/flags; zeroed once, left zero by every completed launch
+  unsigned* sync = nullptr;
+  unsigned epoch = 0;  // reverse flag value of the last call (never 0)
+  int plan = -1;       // JWV_PLAN_* bits; -1 = env defaults
   // profiling: hipEvent pairs around every kernel launch on the launch stream
   bool prof = false;
   int prof_only = -1;  // -1: every kind; else one KernelKind
@@ -145,12 +150,12 @@ void hipchk(hipError_t e, const char* what) {
 enum KernelKind {
   K_FWT_FWD_TILE, K_FWT_FWD_RES, K_FWT_REV_TILE, K_FWT_REV_RES, K_WPT_FWD_TILE, K_WPT_FWD_RES,
   K_WPT_REV_TILE, K_WPT_REV_RES, K_MODWT_FWD_TILE, K_MODWT_FWD_LEVEL, K_MODWT_INV_TILE,
-  K_MODWT_INV_LEVEL, K_COPY, K_NKINDS
+  K_MODWT_INV_LEVEL, K_COPY, K_FWT_FWD_CHAIN, K_FWT_REV_CHAIN, K_FWT_REV_HEAD, K_NKINDS
 };
 const char* const kKindNames[K_NKINDS] = {
     "fwt_fwd_tile", "fwt_fwd_res", "fwt_rev_tile", "fwt_rev_res", "wpt_fwd_tile", "wpt_fwd_res",
     "wpt_rev_tile", "wpt_rev_res", "modwt_fwd_tile", "modwt_fwd_level", "modwt_inv_tile",
-    "modwt_inv_level", "copy_axis"};
+    "modwt_inv_level", "copy_axis", "fwt_fwd_chain", "fwt_rev_chain", "fwt_rev_head"};
 
 hipEvent_t take_event(jwv_ctx* c) {
   if (!c->ev_pool.empty()) {
@@ -240,9 +245,59 @@ bool fast1(const Bank& b, const Axis& a, bool rev) {
   return true;
 }
 
+// ----------------------------------------------------------- FWT chains
+// One launch per direction for a single long contiguous signal
+// (fwt1_chain.hpp): the planner's tiled passes and resident tail become roles
+// of one grid.  Only where the compiled role geometry (jwv::ChainGeo) covers
+// the whole level plan; everything else takes the multi-launch plan below.
+using jwv::ChainGeo;
+
+unsigned* sync_words(jwv_ctx* c) {
+  if (!c->sync) {
+    HIPCHK(hipMalloc(&c->sync, 2 * ChainGeo::kWords * sizeof(unsigned)));
+    HIPCHK(hipMemsetAsync(c->sync, 0, 2 * ChainGeo::kWords * sizeof(unsigned), c->stream));
+  }
+  return c->sync;
+}
+
+int plan_of(jwv_ctx* c) { return c->plan >= 0 ? c->plan : ChainGeo::default_plan(); }
+
+bool try_fwd_chain(jwv_ctx* c, const Bank& b, const Axis& a, int nlev) {
+  if (!(plan_of(c) & JWV_PLAN_CHAIN_FWD) || a.outer != 1 || !fast1(b, a, false)) return false;
+  const int64_t h = a.len, hB = h >> ChainGeo::kKA, hC = hB >> ChainGeo::kKB;
+  const int64_t mB = ChainGeo::kTB + (int64_t)(b.L - 2) * ((1 << ChainGeo::kKB) - 1);
+  const int levC = nlev - ChainGeo::kKA - ChainGeo::kKB;
+  if (levC < 0 || h % ChainGeo::kTAf || hB % ChainGeo::kTB || mB > hB || hC > ChainGeo::kCap)
+    return false;
+  if (hB / ChainGeo::kTB + 1 > ChainGeo::kWords) return false;
+  double* wsA = grow(c, c->ws[0], (size_t)hB);
+  double* wsB = grow(c, c->ws[1], (size_t)hC);
+  jwv::ChainFwdArgs ca{a.src, a.dst, wsA, wsB, sync_words(c), (int)h, levC};
+  { ProfScope ps_(c, K_FWT_FWD_CHAIN, 16.0 * h);
+    hipchk(jwv::launch_fwt_fwd_chain(b, use_fma(c), ca, c->stream), "fwt_fwd_chain"); }
+  return true;
+}
+
+bool try_rev_chain(jwv_ctx* c, const Bank& b, const Axis& a, int h0) {
+  if (!(plan_of(c) & JWV_PLAN_CHAIN_REV) || a.outer != 1 || !fast1(b, a, true)) return false;
+  const int64_t h = a.len, hM = h >> ChainGeo::kKAr, hR = hM >> ChainGeo::kKM;
+  if (hM % ChainGeo::kTM || hR < 64 || hR > ChainGeo::kCap || h0 > hR) return false;
+  if (2 + hM / ChainGeo::kTM > ChainGeo::kWords) return false;
+  const int nR = exponent(hR / h0) + 1;
+  double* wsR = grow(c, c->ws[0], (size_t)hR);
+  double* wsM = grow(c, c->ws[1], (size_t)hM);
+  if (++c->epoch == 0) c->epoch = 1;
+  jwv::ChainRevArgs ca{a.src, a.dst, wsR, wsM, sync_words(c) + ChainGeo::kWords, (int)h, h0, nR,
+                       c->epoch};
+  { ProfScope ps_(c, K_FWT_REV_CHAIN, 16.0 * h);
+    hipchk(jwv::launch_fwt_rev_chain(b, use_fma(c), ca, c->stream), "fwt_rev_chain"); }
+  return true;
+}
+
 void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
   const int nlev = fwd_levels(a.len, b.tw, level);
   if (nlev == 0) return copy_axis(c, a);
+  if (try_fwd_chain(c, b, a, nlev)) return;
   const int C = col_slab(a.inner), cap = Geo::res_cap(C), KM = Geo::fwt_k(C);
   const bool f1 = fast1(b, a, false);
   // levels of the tiled pass at level-input size h: KM, except that on the
@@ -293,6 +348,7 @@ void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
 void fwt_rev_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
   const int h = rev_first(a.len, b.tw, level);
   if (h == 0) return copy_axis(c, a);
+  if (try_rev_chain(c, b, a, h)) return;
   const int C = col_slab(a.inner);
   // fwt1 path, signal longer than one resident block: the resident tail stops
   // at kFwt1RevTail and the tiled passes take up to kFwt1KMax levels
@@ -321,7 +377,25 @@ void fwt_rev_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
   const double* acur;
   AxisView acv;
   int h1, pp = 0;
-  if (h <= cap) {
+  // JWV_PLAN_REV_HEAD: the resident pass and the first tiled pass (kFwt1KMax
+  // levels, fwt1 geometry) fused into one launch (fwt_rev_head1); the
+  // remaining tiled passes follow as below.
+  if (f1 && h <= cap && a.outer == 1 && (plan_of(c) & JWV_PLAN_REV_HEAD) &&
+      cap == Geo::kFwt1RevTail && Geo::kFwt1KMax == ChainGeo::kKM &&
+      ((int64_t)cap << ChainGeo::kKM) <= a.len) {
+    const int hM = cap << ChainGeo::kKM;
+    const bool last = hM == a.len;
+    double* out = last ? a.dst : c->ws[1].p;
+    if (++c->epoch == 0) c->epoch = 1;
+    jwv::RevHeadArgs ra{a.src, out, c->ws[0].p, sync_words(c) + ChainGeo::kWords, h,
+                        exponent(cap / h) + 1, c->epoch};
+    { ProfScope ps_(c, K_FWT_REV_HEAD, 16.0 * hM);
+      hipchk(jwv::launch_fwt_rev_head(b, use_fma(c), ra, c->stream), "fwt_rev_head"); }
+    if (last) return;
+    acur = out;
+    acv = cview(hM, 1);
+    h1 = hM * 2;
+  } else if (h <= cap) {
     const int hres = std::min(a.len, cap);
     const int nres = exponent(hres / h) + 1;
     const bool last = hres == a.len;
@@ -731,6 +805,19 @@ bool Geo::rev_pref() {
 }
 #define JWV_MODE2(name, ...) \
   return fma ? fused::name(__VA_ARGS__) : exact::name(__VA_ARGS__)
+int ChainGeo::default_plan() {
+  static const int p = env_int("JWV_PLAN", JWV_PLAN_REV_HEAD) & 7;
+  return p;
+}
+hipError_t launch_fwt_rev_head(const Bank& b, bool fma, const RevHeadArgs& a, hipStream_t s) {
+  JWV_MODE2(fwt_rev_head, b, a, s);
+}
+hipError_t launch_fwt_fwd_chain(const Bank& b, bool fma, const ChainFwdArgs& a, hipStream_t s) {
+  JWV_MODE2(fwt_fwd_chain, b, a, s);
+}
+hipError_t launch_fwt_rev_chain(const Bank& b, bool fma, const ChainRevArgs& a, hipStream_t s) {
+  JWV_MODE2(fwt_rev_chain, b, a, s);
+}
 hipError_t launch_fwt_fwd_res(const Bank& b, bool fma, int C, const ResArgs& a, hipStream_t s) {
   hipError_t e = hipSuccess;
   if (C == 1 && (fma ? fused::fwt_fwd_res1(b, a, s, e) : exact::fwt_fwd_res1(b, a, s, e)))
@@ -822,6 +909,7 @@ int jwv_ctx_destroy(jwv_ctx* c) {
   hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->ws[0], &c->ws[1], &c->big, &c->big2, &c->red, &c->hin, &c->hout})
     if (b->p) hipFree(b->p);
+  if (c->sync) hipFree(c->sync);
   for (auto& r : c->recs) { hipEventDestroy(r.e0); hipEventDestroy(r.e1); }
   for (auto e : c->ev_pool) hipEventDestroy(e);
   if (c->own) hipStreamDestroy(c->own);
@@ -855,8 +943,28 @@ int jwv_ctx_set_math(jwv_ctx* c, int mode) {
   return JWV_OK;
 }
 
+int jwv_ctx_set_plan(jwv_ctx* c, int flags) {
+  if (!c) return set_err(nullptr, JWV_ERR_BAD_CALL, "ctx is NULL");
+  if (flags & ~(JWV_PLAN_CHAIN_REV | JWV_PLAN_CHAIN_FWD | JWV_PLAN_REV_HEAD))
+    return set_err(c, JWV_ERR_BAD_CALL, "unknown plan flag");
+  c->plan = flags;
+  return JWV_OK;
+}
+
 int jwv_ctx_synchronize(jwv_ctx* c) {
-  return guarded(c, [&] { hipchk(hipStreamSynchronize(c->stream), "sync"); });
+  return guarded(c, [&] {
+    hipchk(hipStreamSynchronize(c->stream), "sync");
+    if (c->sync) {  // reverse chain timeout word (fwt1_chain.hpp)
+      unsigned* tmo = c->sync + ChainGeo::kWords;
+      unsigned v = 0;
+      hipchk(hipMemcpy(&v, tmo, sizeof(v), hipMemcpyDeviceToHost), "sync word");
+      if (v) {
+        hipchk(hipMemset(tmo, 0, sizeof(v)), "sync word");
+        throw Fail{JWV_ERR_DEVICE, "chained reverse FWT: an in-kernel wait timed out (grid not "
+                                   "co-resident?); results of that call are invalid"};
+      }
+    }
+  });
 }
 
 int jwv_ctx_profile_enable(jwv_ctx* c, int on) {

@@ -35,7 +35,7 @@ struct Fwd1Geo {
   }
 };
 
-template <int L, int NT, int T, int K, bool FMA, int l>
+template <int L, int NT, int T, int K, bool FMA, int l, bool WT = false>
 struct Fwd1Level {
   // level l reads the level-(l-1) window at lds + off(l-1) (l = 1: lds) and
   // writes its approximations at lds + off(l) (the last level: ya).
@@ -70,8 +70,8 @@ struct Fwd1Level {
         fwd_pair<L, FMA>(tp, [&](int j) { return x[j]; }, a0, d0);
         fwd_pair<L, FMA>(tp, [&](int j) { return x[j + 2]; }, a1, d1);
         const int p = 2 * q;
-        if constexpr (l == K) {
-          *reinterpret_cast<double2*>(ya + (int64_t)t * own + p) = make_double2(a0, a1);
+        if constexpr (l == K) {  // WT: handed to another workgroup of this launch
+          st2<WT>(ya + (int64_t)t * own + p, a0, a1);
         } else if constexpr (l == 1) {
           av[r] = make_double2(a0, a1);  // in place: written after every wave has read
         } else {
@@ -94,7 +94,7 @@ struct Fwd1Level {
         }
       }
       lds_barrier();
-      Fwd1Level<L, NT, T, K, FMA, l + 1>::run(tp, lds, yd0, hl >> 1, t, ya);
+      Fwd1Level<L, NT, T, K, FMA, l + 1, WT>::run(tp, lds, yd0, hl >> 1, t, ya);
     }
   }
 };
@@ -154,7 +154,7 @@ struct Rev1Geo {
   static_assert(((T >> K) & 1) == 0, "T/2^K must be even");
 };
 
-template <int L, int NT, int T, int K, bool FMA, int l>
+template <int L, int NT, int T, int K, bool FMA, int l, bool WT = false>
 struct Rev1Level {
   __device__ __forceinline__ static void run(const RevTaps<L>& tp, double* lds, int t,
                                              double* __restrict__ y) {
@@ -185,8 +185,8 @@ struct Rev1Level {
                 tp, mg, [=](int q) { return ab[li - q]; }, [=](int q) { return db[li - q]; }, xe,
                 xo);
         }
-        if constexpr (l == 0) {
-          *reinterpret_cast<double2*>(y + (int64_t)t * T + 2 * ml) = make_double2(xe, xo);
+        if constexpr (l == 0) {  // WT: handed to another workgroup of this launch
+          st2<WT>(y + (int64_t)t * T + 2 * ml, xe, xo);
         } else {
           *reinterpret_cast<double2*>(ob + 2 * ml) = make_double2(xe, xo);
         }
@@ -194,7 +194,7 @@ struct Rev1Level {
     }
     if constexpr (l > 0) {
       lds_barrier();
-      Rev1Level<L, NT, T, K, FMA, l - 1>::run(tp, lds, t, y);
+      Rev1Level<L, NT, T, K, FMA, l - 1, WT>::run(tp, lds, t, y);
     }
   }
 };

@@ -25,6 +25,7 @@ __device__ __forceinline__ void fwd_pair_wrap(const FwdTaps<L>& tp, const double
 #pragma unroll
   for (int j = 0; j < L; ++j) x[j] = in[(2 * p + j) & msk];
   fwd_pair<L, FMA>(tp, [&](int j) { return x[j]; }, a, d);
+  pin2(a, d);
 }
 
 // Synthesis pair m of a level of size h >= L: a = lds[0, half), d =
@@ -48,6 +49,7 @@ __device__ __forceinline__ void rev_pair_wrap(const RevTaps<L>& tp, const double
   if (m < Q - 1)
     rev_pair_head<L, FMA>(tp, m, [&](int q) { return av[q]; }, [&](int q) { return dv[q]; }, xe,
                           xo);
+  pin2(xe, xo);
 }
 
 // Levels with h < L wrap several times: Wavelet.reverse's scatter order
@@ -75,21 +77,13 @@ __device__ __forceinline__ double rev_small_regs(const RevTaps<L>& tp, const dou
 // dst row: coefficient array (details of level size h at dst[h/2, h), final
 // approximation at dst[0, h_end)).
 // ====================================================================
+// Levels of the resident forward on a level input already in lds[0, h0):
+// details to y[h/2, h) per level, the final approximation to y[0, h_end).
 template <int L, int NT, int CAP, bool FMA>
-__global__ __launch_bounds__(NT) void fwt_fwd_res1(const double* __restrict__ src, int64_t s_src,
-                                                   double* __restrict__ dst, int64_t s_dst, int h0,
-                                                   int nlev, FwdTaps<L> tp) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
+__device__ __forceinline__ void fwd_res1_levels(double* lds, double* __restrict__ y, int h0,
+                                                int nlev, const FwdTaps<L>& tp) {
   constexpr int RM = CAP / 2 / NT > 0 ? CAP / 2 / NT : 1;
-  const int64_t o = blockIdx.x;
-  double* __restrict__ y = dst + o * s_dst;
   const int tid = threadIdx.x;
-  JWV_STAMP(0);
-  load_window<1, NT, (CAP + NT - 1) / NT>(lds, src + o * s_src, h0, true, 0, 1,
-                                          [&](int e) { return (int64_t)e; });
-  dma_fence_barrier();
-  JWV_STAMP(1);
-
   int h = h0, lev = 0;
   // block-wide levels: np = h/2 > 64 pairs, a power of two
   for (; lev < nlev && (h >> 1) > 64; ++lev, h >>= 1) {
@@ -154,25 +148,32 @@ __global__ __launch_bounds__(NT) void fwt_fwd_res1(const double* __restrict__ sr
   JWV_STAMP(42);
 }
 
+template <int L, int NT, int CAP, bool FMA>
+__global__ __launch_bounds__(NT) void fwt_fwd_res1(const double* __restrict__ src, int64_t s_src,
+                                                   double* __restrict__ dst, int64_t s_dst, int h0,
+                                                   int nlev, FwdTaps<L> tp) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int64_t o = blockIdx.x;
+  JWV_STAMP(0);
+  load_window<1, NT, (CAP + NT - 1) / NT>(lds, src + o * s_src, h0, true, 0, 1,
+                                          [&](int e) { return (int64_t)e; });
+  dma_fence_barrier();
+  JWV_STAMP(1);
+  fwd_res1_levels<L, NT, CAP, FMA>(lds, dst + o * s_dst, h0, nlev, tp);
+}
+
 // ====================================================================
 // Reverse, resident, C = 1.  src row: coefficient prefix [0, htop) with
 // htop = h0 << (nlev-1) (h0 = first synthesis level size); dst row: [0, htop).
 // ====================================================================
+// Levels of the resident reverse on the coefficient prefix already in
+// lds[0, htop), htop = h0 << (nlev-1); the result is left in lds[0, htop)
+// (the caller stores it; ends with a block barrier).
 template <int L, int NT, int CAP, bool FMA>
-__global__ __launch_bounds__(NT) void fwt_rev_res1(const double* __restrict__ src, int64_t s_src,
-                                                   double* __restrict__ dst, int64_t s_dst, int h0,
-                                                   int nlev, RevTaps<L> tp) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
+__device__ __forceinline__ void rev_res1_levels(double* lds, int h0, int nlev,
+                                                const RevTaps<L>& tp) {
   constexpr int RM = CAP / 2 / NT > 0 ? CAP / 2 / NT : 1;
-  const int64_t o = blockIdx.x;
   const int tid = threadIdx.x;
-  const int htop = nlev > 0 ? (h0 << (nlev - 1)) : h0;
-  JWV_STAMP(0);
-  load_window<1, NT, (CAP + NT - 1) / NT>(lds, src + o * s_src, htop, true, 0, 1,
-                                          [&](int e) { return (int64_t)e; });
-  dma_fence_barrier();
-  JWV_STAMP(1);
-
   int h = h0, lev = 0;
   if (nlev > 0 && (h >> 1) <= 64) {  // small levels: wave 0 alone
     if (tid < 64) {
@@ -240,6 +241,22 @@ __global__ __launch_bounds__(NT) void fwt_rev_res1(const double* __restrict__ sr
     }
     lds_barrier();
   }
+}
+
+template <int L, int NT, int CAP, bool FMA>
+__global__ __launch_bounds__(NT) void fwt_rev_res1(const double* __restrict__ src, int64_t s_src,
+                                                   double* __restrict__ dst, int64_t s_dst, int h0,
+                                                   int nlev, RevTaps<L> tp) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int64_t o = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int htop = nlev > 0 ? (h0 << (nlev - 1)) : h0;
+  JWV_STAMP(0);
+  load_window<1, NT, (CAP + NT - 1) / NT>(lds, src + o * s_src, htop, true, 0, 1,
+                                          [&](int e) { return (int64_t)e; });
+  dma_fence_barrier();
+  JWV_STAMP(1);
+  rev_res1_levels<L, NT, CAP, FMA>(lds, h0, nlev, tp);
   JWV_STAMP(40);
   double* __restrict__ y = dst + o * s_dst;
   for (int q = 2 * tid; q < htop; q += 2 * NT)

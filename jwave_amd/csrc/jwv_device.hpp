@@ -205,6 +205,104 @@ __device__ __forceinline__ int opaque_tid() {
   return t;
 }
 
+// ---------------------------------------------------------------------------
+// In-launch hand-off between workgroups (chained kernels, fwt1_chain.hpp).
+// gfx950 L1s are per CU and never refreshed by other CUs' stores; the XCD L2s
+// are kept coherent for hipMalloc memory only for write-through data.  The
+// protocol (MI355X_MICROARCH.md, inter-workgroup visibility):
+//   producer: handed-off bytes stored write-through (sc1) -> every storing
+//             wave `s_waitcnt vmcnt(0)` -> workgroup barrier -> ONE lane
+//             signals with an agent-scope atomic (counter add or flag store);
+//   consumer: ONE lane polls relaxed (sc1 loads) or reads its add's return
+//             value -> that lane's agent-scope acquire (buffer_inv sc1) ->
+//             `s_waitcnt vmcnt(0)` -> workgroup barrier -> plain / LDS-DMA loads.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void st_wt(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
+                     __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+// Two adjacent doubles (16-B aligned p): one 16-B store, or two sc1 stores.
+template <bool WT>
+__device__ __forceinline__ void st2(double* p, double a, double b) {
+  if constexpr (WT) {
+    st_wt(p, a);
+    st_wt(p + 1, b);
+  } else {
+    *reinterpret_cast<double2*>(p) = make_double2(a, b);
+  }
+}
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ unsigned atomic_add_agent(unsigned* p, unsigned v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void store_agent(unsigned* p, unsigned v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned load_agent(const unsigned* p) {
+  return __hip_atomic_load(const_cast<unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_wt(const double* p) {
+  return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<unsigned long long*>(
+                                                          const_cast<double*>(p)),
+                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+// Window of W handed-off doubles (lds[e] = src[rowoff(e)]) read with sc1
+// loads (L1 bypass) into registers, then LDS: with the producer's sc1 stores
+// and the signal read before, no acquire is needed.  All MAXU loads are in
+// flight at once.  Caller issues lds_barrier().
+template <int NT, int MAXU, typename RowOff>
+__device__ __forceinline__ void load_window_wt(double* lds, const double* src, int W,
+                                               RowOff rowoff) {
+  const int tid = threadIdx.x;
+  double v[MAXU];
+#pragma unroll
+  for (int r = 0; r < MAXU; ++r) {
+    const int e = tid + r * NT;
+    if (e < W) v[r] = ld_wt(src + rowoff(e));
+  }
+#pragma unroll
+  for (int r = 0; r < MAXU; ++r) {
+    const int e = tid + r * NT;
+    if (e < W) lds[e] = v[r];
+  }
+}
+// Acquire for the whole workgroup: lane 0 invalidates this CU's L1, its wait
+// holds the barrier until the invalidate has completed.
+__device__ __forceinline__ void block_acquire() {
+  if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+// Bounded relaxed poll of one flag (one lane).  Never spins forever: after
+// ~2^22 polls it records a timeout and gives up (results are then wrong, the
+// host reports the timeout word; the grid still drains).
+__device__ __forceinline__ void poll_eq(const unsigned* f, unsigned v, unsigned* tmo) {
+  for (unsigned i = 0; i < (1u << 22); ++i) {
+    if (load_agent(f) == v) return;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  store_agent(tmo, 1u);
+}
+
+// Wave-wide bounded poll until every flag f[0, n) equals v (one wave).
+__device__ __forceinline__ void poll_all(const unsigned* f, int n, unsigned v, unsigned* tmo) {
+  const int lane = threadIdx.x & 63;
+  for (unsigned i = 0; i < (1u << 22); ++i) {
+    bool ok = true;
+    for (int k = lane; k < n; k += 64) ok = ok && load_agent(f + k) == v;
+    if (__all(ok)) return;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  if (lane == 0) store_agent(tmo, 1u);
+}
+
+// Materialise two results here: stops the compiler from sinking their
+// computation into later exec-masked stores, where two independent FP64
+// accumulation chains would run one after the other instead of interleaved
+// (latency-bound tail levels: ~2x per level).
+__device__ __forceinline__ void pin2(double& a, double& b) { asm volatile("" : "+v"(a), "+v"(b)); }
+
 template <bool FMA>
 __device__ __forceinline__ double mac(double acc, double a, double b) {
   if constexpr (FMA) {

@@ -94,6 +94,41 @@ struct Geo {
   static int wpt_k(int C) { return C == 1 ? kWptK1 : kWptK8; }
 };
 
+// Single-launch FWT chains (fwt1_chain.hpp): geometry of the compiled roles.
+// Forward: A tiles (kTAf, kKA) -> B units (kTB, kKB) -> resident C (<= kCap).
+// Reverse: resident R (<= kCap) -> M units (kTM, kKM) -> A tiles (kTA, kKAr).
+struct ChainGeo {
+  static constexpr int kTAf = 4096, kKA = 6, kTB = 2048, kKB = 7, kCap = 2048;
+  static constexpr int kTA = 2048;
+  static constexpr int kTM = 2048, kKM = 9, kKAr = 5;
+  static constexpr int kWords = 4096;  // sync words per direction (ctx buffer: 2x)
+  static int default_plan();          // JWV_PLAN_* bits: env JWV_PLAN, default REV_HEAD
+};
+struct ChainFwdArgs {
+  const double* src; double* dst;
+  double* wsA; double* wsB;   // h >> kKA, h >> (kKA + kKB) doubles
+  unsigned* cnt;              // >= nU + 1 words, zero between calls
+  int h, levC;
+};
+struct ChainRevArgs {
+  const double* coef; double* dst;
+  double* wsR; double* wsM;   // hR, hR << kKM doubles
+  unsigned* ctl;              // >= 2 + nM words
+  int h, h0R, nR;
+  unsigned epoch;             // != 0, new per call
+};
+struct RevHeadArgs {  // fwt_rev_head1: R + M units in one launch
+  const double* coef;
+  double* wsM;                // hR << kKM doubles (read by the next launch)
+  double* wsR;                // hR doubles
+  unsigned* ctl;              // 2 words: timeout, R flag
+  int h0R, nR;
+  unsigned epoch;
+};
+hipError_t launch_fwt_rev_head(const Bank&, bool fma, const RevHeadArgs&, hipStream_t);
+hipError_t launch_fwt_fwd_chain(const Bank&, bool fma, const ChainFwdArgs&, hipStream_t);
+hipError_t launch_fwt_rev_chain(const Bank&, bool fma, const ChainRevArgs&, hipStream_t);
+
 // Each returns hipSuccess or the launch error.  `fma` selects the math mode.
 hipError_t launch_fwt_fwd_res(const Bank&, bool fma, int C, const ResArgs&, hipStream_t);
 hipError_t launch_fwt_rev_res(const Bank&, bool fma, int C, const ResArgs&, hipStream_t);
@@ -120,6 +155,9 @@ hipError_t launch_compress_magnitude(const double* c, double* y, int64_t n, doub
 // Per-mode entry points implemented by launch_{fwt,wpt,modwt}.hip compiled
 // twice (JWV_FMA=0 / 1).
 namespace exact {
+hipError_t fwt_rev_head(const Bank&, const RevHeadArgs&, hipStream_t);
+hipError_t fwt_fwd_chain(const Bank&, const ChainFwdArgs&, hipStream_t);
+hipError_t fwt_rev_chain(const Bank&, const ChainRevArgs&, hipStream_t);
 // fwt1 kernels: return false when the case is not covered (nothing launched)
 bool wpt_tile1(const Bank&, const TileArgs&, hipStream_t, bool fwd, hipError_t& err);
 bool fwt_fwd_res1(const Bank&, const ResArgs&, hipStream_t, hipError_t& err);
@@ -138,6 +176,9 @@ hipError_t modwt_fwd(const Bank&, bool tiled, const ModwtArgs&, hipStream_t);
 hipError_t modwt_inv(const Bank&, bool tiled, const ModwtArgs&, hipStream_t);
 }  // namespace exact
 namespace fused {
+hipError_t fwt_rev_head(const Bank&, const RevHeadArgs&, hipStream_t);
+hipError_t fwt_fwd_chain(const Bank&, const ChainFwdArgs&, hipStream_t);
+hipError_t fwt_rev_chain(const Bank&, const ChainRevArgs&, hipStream_t);
 // fwt1 kernels: return false when the case is not covered (nothing launched)
 bool wpt_tile1(const Bank&, const TileArgs&, hipStream_t, bool fwd, hipError_t& err);
 bool fwt_fwd_res1(const Bank&, const ResArgs&, hipStream_t, hipError_t& err);

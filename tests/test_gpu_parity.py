@@ -101,6 +101,33 @@ def test_fwt_batch(ctx, wname):
                          "batch rev")
 
 
+@pytest.mark.parametrize("wname", ["Haar1", "Daubechies2", "Daubechies4", "Daubechies8", "Symlet8"])
+@pytest.mark.parametrize("n", [1 << 18, 1 << 20, 1 << 21])
+def test_fwt_chain(ctx, wname, n):
+    """Pass plans for long single signals (fwt1_chain.hpp: reverse head,
+    whole-direction chains, multi-launch): every level count that switches roles
+    on or off (forward chain from 13 levels, reverse chain when the resident
+    part fits), each call twice in a row so a counter or flag left behind by
+    the first would corrupt the second."""
+    w = jw.by_class(wname)
+    x = rnd(n, n + 1)
+    full = n.bit_length() - 1
+    try:
+        for plan in ({"rev_head"}, {"chain_rev", "chain_fwd"}, set()):
+            ctx.set_plan(plan)
+            for lev in sorted({12, 13, 14, 15, full - 1, full}):
+                yr = oracle.fwt_forward(w, x, lev)
+                tag = "%s n=%d l=%d plan=%s" % (wname, n, lev, sorted(plan))
+                for rep in range(2):
+                    assert_exact(T.fwt_forward(x, w, lev, ctx), yr, "fwd %s #%d" % (tag, rep))
+                xr = oracle.fwt_reverse(w, yr, lev)
+                for rep in range(2):
+                    assert_exact(T.fwt_reverse(yr, w, lev, ctx), xr, "rev %s #%d" % (tag, rep))
+            ctx.synchronize()  # raises if a chained wait timed out
+    finally:
+        ctx.set_plan()
+
+
 def test_fwt_config2_full_size(ctx):
     """Config 2: Daubechies4, N = 2^24, full depth — exact vs oracle, and the
     round trip vs the input (reported bound from the taps' precision)."""

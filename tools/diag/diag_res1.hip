@@ -27,14 +27,14 @@ int main() {
     float ms;
     hipMemcpyToSymbol(HIP_SYMBOL(jwv_stamps), z, sizeof(z));
     hipEventRecord(a);
-    hipLaunchKernelGGL((fwt_fwd_res1<8, 1024, 8192, false>), dim3(1), dim3(1024), 4096 * 8 + 16, 0, x, 0, y, 0, 4096, 12, tf);
+    hipLaunchKernelGGL((fwt_fwd_res1<8, 1024, 8192, false>), dim3(1), dim3(1024), 512 * 8 + 16, 0, x, 0, y, 0, 512, 9, tf);
     hipEventRecord(b); hipEventSynchronize(b); hipEventElapsedTime(&ms, a, b);
-    if (rep >= 2) show("fwd_res1 4096/12", ms);
+    if (rep >= 2) show("fwd_res1 512/9", ms);
     hipMemcpyToSymbol(HIP_SYMBOL(jwv_stamps), z, sizeof(z));
     hipEventRecord(a);
-    hipLaunchKernelGGL((fwt_rev_res1<8, 1024, 8192, false>), dim3(1), dim3(1024), 8192 * 8 + 16, 0, x, 0, y, 0, 2, 13, tr);
+    hipLaunchKernelGGL((fwt_rev_res1<8, 1024, 8192, false>), dim3(1), dim3(1024), 1024 * 8 + 16, 0, x, 0, y, 0, 2, 10, tr);
     hipEventRecord(b); hipEventSynchronize(b); hipEventElapsedTime(&ms, a, b);
-    if (rep >= 2) show("rev_res1 2/13   ", ms);
+    if (rep >= 2) show("rev_res1 2/10   ", ms);
   }
   return 0;
 }

@@ -18,6 +18,8 @@ CASES = {
     "fwt_d4_2^24": ("fwt", "Daubechies4", 1, 1 << 24, 24),
     "fwt_d4_4096": ("fwt", "Daubechies4", 1, 4096, 12),
     "fwt_d4_2^18": ("fwt", "Daubechies4", 1, 1 << 18, 18),
+    "fwt_d4_2^20": ("fwt", "Daubechies4", 1, 1 << 20, 20),
+    "fwt_d4_2^22": ("fwt", "Daubechies4", 1, 1 << 22, 22),
     "fwt_d4_b64x65536": ("fwt", "Daubechies4", 64, 1 << 16, 16),
     "fwt_d8_rows8192": ("fwt", "Daubechies8", 8192, 8192, 13),
     "wpt_s8_b512x65536": ("wpt", "Symlet8", 512, 1 << 16, 6),
