@@ -150,12 +150,18 @@ void hipchk(hipError_t e, const char* what) {
 enum KernelKind {
   K_FWT_FWD_TILE, K_FWT_FWD_RES, K_FWT_REV_TILE, K_FWT_REV_RES, K_WPT_FWD_TILE, K_WPT_FWD_RES,
   K_WPT_REV_TILE, K_WPT_REV_RES, K_MODWT_FWD_TILE, K_MODWT_FWD_LEVEL, K_MODWT_INV_TILE,
-  K_MODWT_INV_LEVEL, K_COPY, K_FWT_FWD_CHAIN, K_FWT_REV_CHAIN, K_FWT_REV_HEAD, K_NKINDS
+  K_MODWT_INV_LEVEL, K_COPY, K_FWT_FWD_CHAIN, K_FWT_REV_CHAIN, K_FWT_REV_HEAD,
+  K_FWT_FWD_TILE_DEEP, K_FWT_REV_TILE_DEEP, K_NKINDS
 };
+// *_tile: the tiled pass that reads (forward) or writes (reverse) the full-length
+// axis — the HBM-bound launch; *_tile_deep: tiled passes over an intermediate
+// approximation (1/2^K of the bytes or less; latency-bound).  They are separate
+// kernel instantiations (different fused level counts), as in rocprofv3.
 const char* const kKindNames[K_NKINDS] = {
     "fwt_fwd_tile", "fwt_fwd_res", "fwt_rev_tile", "fwt_rev_res", "wpt_fwd_tile", "wpt_fwd_res",
     "wpt_rev_tile", "wpt_rev_res", "modwt_fwd_tile", "modwt_fwd_level", "modwt_inv_tile",
-    "modwt_inv_level", "copy_axis", "fwt_fwd_chain", "fwt_rev_chain", "fwt_rev_head"};
+    "modwt_inv_level", "copy_axis", "fwt_fwd_chain", "fwt_rev_chain", "fwt_rev_head",
+    "fwt_fwd_tile_deep", "fwt_rev_tile_deep"};
 
 hipEvent_t take_event(jwv_ctx* c) {
   if (!c->ev_pool.empty()) {
@@ -294,11 +300,24 @@ bool try_rev_chain(jwv_ctx* c, const Bank& b, const Axis& a, int h0) {
   return true;
 }
 
+// Resident-pass cap of an FWT axis transform.  Many contiguous signals (2-D
+// rows, batches) can instead run their top levels through the C = 1 tile
+// kernels and only a short tail resident (config 3 rows: 2.21 -> 1.99 ms per
+// step at 2048).  env JWV_ROWCAP (elements; >= kResCap1 = always resident).
+int fwt_res_cap(int C, int64_t outer) {
+  static const int rowcap = [] {
+    const char* v = std::getenv("JWV_ROWCAP");
+    return v ? std::atoi(v) : 2048;
+  }();
+  if (C == 1 && outer >= 64 && rowcap >= 64 && rowcap < Geo::kResCap1) return rowcap;
+  return Geo::res_cap(C);
+}
+
 void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
   const int nlev = fwd_levels(a.len, b.tw, level);
   if (nlev == 0) return copy_axis(c, a);
   if (try_fwd_chain(c, b, a, nlev)) return;
-  const int C = col_slab(a.inner), cap = Geo::res_cap(C), KM = Geo::fwt_k(C);
+  const int C = col_slab(a.inner), cap = fwt_res_cap(C, a.outer), KM = Geo::fwt_k(C);
   const bool f1 = fast1(b, a, false);
   // levels of the tiled pass at level-input size h: KM, except that on the
   // fwt1 path the pass that ends the tiled part runs on down to kFwt1FwdTail
@@ -330,7 +349,8 @@ void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
     const AxisView av = last ? a.dv : cview(h >> K, a.inner);
     jwv::TileArgs t{cur, cv, nullptr, {}, a.dst, a.dv, ad, av, h, K, a.outer, a.inner,
                     dma_view(cur, cv, C, a.inner)};
-    { ProfScope ps_(c, K_FWT_FWD_TILE, 16.0 * a.outer * h * a.inner);
+    { ProfScope ps_(c, h == a.len ? K_FWT_FWD_TILE : K_FWT_FWD_TILE_DEEP,
+                    16.0 * a.outer * h * a.inner);
     hipchk(jwv::launch_fwt_fwd_tile(b, use_fma(c), C, t, c->stream), "fwt_fwd_tile"); }
     cur = ad;
     cv = av;
@@ -352,7 +372,7 @@ void fwt_rev_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
   const int C = col_slab(a.inner);
   // fwt1 path, signal longer than one resident block: the resident tail stops
   // at kFwt1RevTail and the tiled passes take up to kFwt1KMax levels
-  const bool f1 = fast1(b, a, true) && a.len > Geo::res_cap(C);
+  const bool f1 = fast1(b, a, true) && a.len > fwt_res_cap(C, a.outer);
   const int cap = f1 ? Geo::kFwt1RevTail : Geo::res_cap(C);
   const int KM = f1 ? Geo::kFwt1KMax : Geo::fwt_k(C);
   // workspace sizing
@@ -423,7 +443,7 @@ void fwt_rev_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
     const AxisView ov = last ? a.dv : cview(hK, a.inner);
     jwv::TileArgs t{acur, acv, a.src, a.sv, out, ov, nullptr, {}, h1, K, a.outer, a.inner,
                     dma_view(acur, acv, C, a.inner) && dma_view(a.src, a.sv, C, a.inner)};
-    { ProfScope ps_(c, K_FWT_REV_TILE, 16.0 * a.outer * hK * a.inner);
+    { ProfScope ps_(c, last ? K_FWT_REV_TILE : K_FWT_REV_TILE_DEEP, 16.0 * a.outer * hK * a.inner);
     hipchk(jwv::launch_fwt_rev_tile(b, use_fma(c), C, t, c->stream), "fwt_rev_tile"); }
     acur = out;
     acv = ov;

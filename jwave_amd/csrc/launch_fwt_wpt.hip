@@ -70,9 +70,14 @@ inline unsigned ncb(int inner, int C) { return (unsigned)((inner + C - 1) / C); 
 constexpr int kBigNT = 1024;
 inline bool few_blocks(const ResArgs& a, int C) { return C == 1 && a.nouter * ncb(a.inner, C) < 64; }
 
-template <int L, int C, int NTX>
+// Short rows of a batch (the resident tail under the C = 1 row tile passes)
+// take a CAP = kShortCap instantiation: its slot loops are sized for the row,
+// not for 8192 elements (config 3 row tails: ~4x faster).
+constexpr int kShortCap = 1024;
+
+template <int L, int C, int NTX, int CAPX = cap<C>()>
 hipError_t fwt_fwd_res_nt(const Bank& b, const ResArgs& a, hipStream_t s) {
-  auto k = fwt_fwd_res<L, C, NTX, cap<C>(), kFMA>;
+  auto k = fwt_fwd_res<L, C, NTX, CAPX, kFMA>;
   const size_t lds = (size_t)(a.n + 2) * C * sizeof(double);
   if (hipError_t e = prep(k, lds)) return e;
   const dim3 grid((unsigned)(a.nouter * ncb(a.inner, C)));
@@ -82,13 +87,15 @@ hipError_t fwt_fwd_res_nt(const Bank& b, const ResArgs& a, hipStream_t s) {
 }
 template <int L, int C>
 hipError_t fwt_fwd_res_go(const Bank& b, const ResArgs& a, hipStream_t s) {
-  if constexpr (C == 1)
+  if constexpr (C == 1) {
     if (few_blocks(a, C)) return fwt_fwd_res_nt<L, C, kBigNT>(b, a, s);
+    if (a.n <= kShortCap) return fwt_fwd_res_nt<L, C, NT, kShortCap>(b, a, s);
+  }
   return fwt_fwd_res_nt<L, C, NT>(b, a, s);
 }
-template <int L, int C, int NTX>
+template <int L, int C, int NTX, int CAPX = cap<C>()>
 hipError_t fwt_rev_res_nt(const Bank& b, const ResArgs& a, hipStream_t s) {
-  auto k = fwt_rev_res<L, C, NTX, cap<C>(), kFMA>;
+  auto k = fwt_rev_res<L, C, NTX, CAPX, kFMA>;
   const int htop = a.nlev > 0 ? (a.n << (a.nlev - 1)) : a.n;
   const size_t lds = (size_t)(htop + 2) * C * sizeof(double);
   if (hipError_t e = prep(k, lds)) return e;
@@ -99,8 +106,11 @@ hipError_t fwt_rev_res_nt(const Bank& b, const ResArgs& a, hipStream_t s) {
 }
 template <int L, int C>
 hipError_t fwt_rev_res_go(const Bank& b, const ResArgs& a, hipStream_t s) {
-  if constexpr (C == 1)
+  if constexpr (C == 1) {
     if (few_blocks(a, C)) return fwt_rev_res_nt<L, C, kBigNT>(b, a, s);
+    const int htop = a.nlev > 0 ? (a.n << (a.nlev - 1)) : a.n;
+    if (htop <= kShortCap) return fwt_rev_res_nt<L, C, NT, kShortCap>(b, a, s);
+  }
   return fwt_rev_res_nt<L, C, NT>(b, a, s);
 }
 template <int L, int C, int T>

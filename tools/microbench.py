@@ -23,6 +23,7 @@ CASES = {
     "fwt_d4_b64x65536": ("fwt", "Daubechies4", 64, 1 << 16, 16),
     "fwt_d8_rows8192": ("fwt", "Daubechies8", 8192, 8192, 13),
     "wpt_s8_b512x65536": ("wpt", "Symlet8", 512, 1 << 16, 6),
+    "modwt_d4_1e7": ("modwt", "Daubechies4", 1, 10_000_000, 8),
 }
 
 
@@ -33,11 +34,17 @@ def run(name, math, reps=20):
     ctx.set_stream(None)
     t = _TapsHolder.of(jw.by_class(wn))
     x = torch.rand(b * n, dtype=torch.float64, device="cuda")
-    y = torch.empty_like(x)
-    z = torch.empty_like(x)
     p = lambda a: ctypes.c_void_p(a.data_ptr())  # noqa: E731
-    f = getattr(lib, "jwv_%s_fwd_batch_f64_dev" % op)
-    r = getattr(lib, "jwv_%s_rev_batch_f64_dev" % op)
+    if op == "modwt":
+        y = torch.empty((lev + 1) * n, dtype=torch.float64, device="cuda")
+        fm, im = lib.jwv_modwt_fwd_f64_dev, lib.jwv_modwt_inv_f64_dev
+        f = lambda xi, yo, b_, n_, ld, lv, t_, h_: fm(xi, yo, n_, lv, t_, h_)  # noqa: E731
+        r = lambda yi, zo, b_, n_, ld, lv, t_, h_: im(yi, zo, n_, lv, t_, h_)  # noqa: E731
+    else:
+        y = torch.empty_like(x)
+        f = getattr(lib, "jwv_%s_fwd_batch_f64_dev" % op)
+        r = getattr(lib, "jwv_%s_rev_batch_f64_dev" % op)
+    z = torch.empty_like(x)
     for _ in range(3):
         assert f(p(x), p(y), b, n, n, lev, t, ctx.handle) == 0
         assert r(p(y), p(z), b, n, n, lev, t, ctx.handle) == 0

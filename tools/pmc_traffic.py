@@ -20,7 +20,12 @@ from collections import defaultdict
 
 KINDS = ["fwt_fwd_tile", "fwt_fwd_res", "fwt_rev_tile", "fwt_rev_res", "wpt_fwd_tile",
          "wpt_fwd_res", "wpt_rev_tile", "wpt_rev_res", "modwt_fwd_tile", "modwt_fwd_level",
-         "modwt_inv_tile", "modwt_inv_level", "copy_axis_kernel"]
+         "modwt_inv_tile", "modwt_inv_level", "fwt_rev_head", "fwt_fwd_chain", "fwt_rev_chain",
+         "copy_axis_kernel"]
+# tiled FWT passes: the launch over the full-length axis keeps the kind's name,
+# passes over intermediate approximations (smaller grids) become "<kind>_deep"
+# (the split capi.cpp's profiler uses).
+DEEP_SPLIT = ("fwt_fwd_tile", "fwt_rev_tile")
 
 
 def kind_of(name):
@@ -42,8 +47,14 @@ def read(dirpath, counter):
                     continue
                 k, mode = kind_of(row.get("Kernel_Name", ""))
                 if k:
-                    vals[(k, mode)].append(float(row["Counter_Value"]))
-    return vals
+                    vals[(k, mode, int(row.get("Grid_Size") or 0))].append(float(row["Counter_Value"]))
+    out = defaultdict(list)
+    for (k, mode, grid), vs in vals.items():
+        grids = [g for (k2, m2, g) in vals if k2 == k and m2 == mode]
+        if k in DEEP_SPLIT and grid < max(grids):
+            k = k + "_deep"
+        out[(k, mode)].extend(vs)
+    return out
 
 
 def main():
