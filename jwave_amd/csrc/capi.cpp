@@ -815,6 +815,10 @@ bool Geo::fwt1() {
   static const bool p = env_int("JWV_FWT1", 1) != 0;
   return p;
 }
+bool Geo::fwt8() {
+  static const bool p = env_int("JWV_FWT8", 1) != 0;
+  return p;
+}
 int Geo::stream_ntc() {
   static const int n = env_int("JWV_STREAM_NTC", 512) == 256 ? 256 : 512;
   return n;
@@ -854,6 +858,8 @@ hipError_t launch_fwt_fwd_tile(const Bank& b, bool fma, int C, const TileArgs& a
   hipError_t e = hipSuccess;
   if (C == 1 && (fma ? fused::fwt_fwd_tile1(b, a, s, e) : exact::fwt_fwd_tile1(b, a, s, e)))
     return e;
+  if (C == 8 && (fma ? fused::fwt_tile8(b, a, s, true, e) : exact::fwt_tile8(b, a, s, true, e)))
+    return e;
   // the generic kernels are compiled for at most fwt_k(C) fused levels
   if (a.K > Geo::fwt_k(C)) return hipErrorInvalidValue;
   JWV_MODE2(fwt_fwd_tile, b, C, a, s);
@@ -861,6 +867,8 @@ hipError_t launch_fwt_fwd_tile(const Bank& b, bool fma, int C, const TileArgs& a
 hipError_t launch_fwt_rev_tile(const Bank& b, bool fma, int C, const TileArgs& a, hipStream_t s) {
   hipError_t e = hipSuccess;
   if (C == 1 && (fma ? fused::fwt_rev_tile1(b, a, s, e) : exact::fwt_rev_tile1(b, a, s, e)))
+    return e;
+  if (C == 8 && (fma ? fused::fwt_tile8(b, a, s, false, e) : exact::fwt_tile8(b, a, s, false, e)))
     return e;
   if (a.K > Geo::fwt_k(C)) return hipErrorInvalidValue;
   JWV_MODE2(fwt_rev_tile, b, C, a, s);

@@ -85,6 +85,9 @@ struct Geo {
   // down to kFwt1Tail samples and starts the reverse tile passes above
   // kFwt1Tail * 2, so the single-block tails stay short.
   static bool fwt1();
+  // C = 8 compile-time-geometry column-slab tiles (fwt8_kernels.hpp): env
+  // JWV_FWT8 (default 1)
+  static bool fwt8();
   static constexpr int kFwt1T = 2048, kRev1T = 2048, kFwt1KMax = 9;
   static constexpr int kFwt1FwdTail = 512, kFwt1RevTail = 1024;
   static constexpr int kWpt1T = 4096, kWpt1KMax = 6;  // WPT tiles (wpt1_kernels.hpp)
@@ -164,6 +167,7 @@ bool fwt_fwd_res1(const Bank&, const ResArgs&, hipStream_t, hipError_t& err);
 bool fwt_rev_res1(const Bank&, const ResArgs&, hipStream_t, hipError_t& err);
 bool fwt_fwd_tile1(const Bank&, const TileArgs&, hipStream_t, hipError_t& err);
 bool fwt_rev_tile1(const Bank&, const TileArgs&, hipStream_t, hipError_t& err);
+bool fwt_tile8(const Bank&, const TileArgs&, hipStream_t, bool fwd, hipError_t& err);
 hipError_t fwt_fwd_res(const Bank&, int C, const ResArgs&, hipStream_t);
 hipError_t fwt_rev_res(const Bank&, int C, const ResArgs&, hipStream_t);
 hipError_t fwt_fwd_tile(const Bank&, int C, const TileArgs&, hipStream_t);
@@ -185,6 +189,7 @@ bool fwt_fwd_res1(const Bank&, const ResArgs&, hipStream_t, hipError_t& err);
 bool fwt_rev_res1(const Bank&, const ResArgs&, hipStream_t, hipError_t& err);
 bool fwt_fwd_tile1(const Bank&, const TileArgs&, hipStream_t, hipError_t& err);
 bool fwt_rev_tile1(const Bank&, const TileArgs&, hipStream_t, hipError_t& err);
+bool fwt_tile8(const Bank&, const TileArgs&, hipStream_t, bool fwd, hipError_t& err);
 hipError_t fwt_fwd_res(const Bank&, int C, const ResArgs&, hipStream_t);
 hipError_t fwt_rev_res(const Bank&, int C, const ResArgs&, hipStream_t);
 hipError_t fwt_fwd_tile(const Bank&, int C, const TileArgs&, hipStream_t);

@@ -4,6 +4,7 @@
 // compiled-in tap count; every other case keeps the generic tile kernels.
 #include "fwt1_kernels.hpp"
 #include "fwt1_res.hpp"
+#include "fwt8_kernels.hpp"
 #include "wpt1_kernels.hpp"
 #include "jwv_launch.hpp"
 
@@ -150,6 +151,43 @@ hipError_t wpt1_l(const Bank& b, const TileArgs& a, hipStream_t s, bool fwd) {
   }
 }
 
+// ---- C = 8 column slabs (fwt8_kernels.hpp); tile rows = the generic C = 8
+// tile the planner sizes grids and workspaces for
+constexpr int kT8 = Geo::kFwtT8;
+template <int L, int K>
+hipError_t fwd8_k(const Bank& b, const TileArgs& a, hipStream_t s) {
+  auto k = fwt_fwd_tile8<L, 256, kT8, K, kFMA>;
+  const size_t lds = (size_t)Fwd8Geo<L, kT8, K>::lds_doubles() * sizeof(double);
+  if (hipError_t e = prep1(k, lds)) return e;
+  FwdTaps<L> tp;
+  for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
+  const dim3 grid((unsigned)(a.nouter * (a.inner / 8) * (a.h / kT8)));
+  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a.src, a.sv, a.dst, a.dv, a.adst, a.av, a.h,
+                     a.inner, tp);
+  return hipGetLastError();
+}
+template <int L, int K>
+hipError_t rev8_k(const Bank& b, const TileArgs& a, hipStream_t s) {
+  auto k = fwt_rev_tile8<L, 256, kT8, K, kFMA>;
+  const size_t lds = (size_t)Rev8Geo<L, kT8, K>::lds_doubles() * sizeof(double);
+  if (hipError_t e = prep1(k, lds)) return e;
+  RevTaps<L> tp;
+  for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
+  const int hK = a.h << (a.K - 1);
+  const dim3 grid((unsigned)(a.nouter * (a.inner / 8) * (hK / kT8)));
+  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a.src, a.sv, a.coef, a.cv, a.dst, a.dv, hK,
+                     a.inner, tp);
+  return hipGetLastError();
+}
+template <int L>
+hipError_t tile8_l(const Bank& b, const TileArgs& a, hipStream_t s, bool fwd) {
+  switch (a.K) {
+    case 1: return fwd ? fwd8_k<L, 1>(b, a, s) : rev8_k<L, 1>(b, a, s);
+    case 2: return fwd ? fwd8_k<L, 2>(b, a, s) : rev8_k<L, 2>(b, a, s);
+    default: return fwd ? fwd8_k<L, 3>(b, a, s) : rev8_k<L, 3>(b, a, s);
+  }
+}
+
 bool plain(const AxisView& v) { return v.pk == 1 && v.s_len == 1; }
 // packet views: stride-1 samples, even strides (16-B aligned packet rows)
 bool pk_ok(const AxisView& v) {
@@ -212,6 +250,22 @@ bool wpt_tile1(const Bank& b, const TileArgs& a, hipStream_t s, bool fwd, hipErr
     case 4: err = wpt1_l<4>(b, a, s, fwd); return true;
     case 8: err = wpt1_l<8>(b, a, s, fwd); return true;
     case 16: err = wpt1_l<16>(b, a, s, fwd); return true;
+    default: return false;
+  }
+}
+// C = 8 slabs: every row segment 16-B aligned (a.dma), whole slabs, a
+// compiled-in tap count, at most Geo::kFwtK8 levels (the generic bound).
+bool fwt_tile8(const Bank& b, const TileArgs& a, hipStream_t s, bool fwd, hipError_t& err) {
+  if (!Geo::fwt8() || !a.dma || a.inner % 8 || a.K < 1 || a.K > 3 || a.K > Geo::kFwtK8)
+    return false;
+  if (!fwd && b.scale != 1.0) return false;
+  const int64_t hT = fwd ? (int64_t)a.h : ((int64_t)a.h << (a.K - 1));
+  if (hT < kT8 || hT % kT8) return false;
+  switch (b.L) {
+    case 2: err = tile8_l<2>(b, a, s, fwd); return true;
+    case 4: err = tile8_l<4>(b, a, s, fwd); return true;
+    case 8: err = tile8_l<8>(b, a, s, fwd); return true;
+    case 16: err = tile8_l<16>(b, a, s, fwd); return true;
     default: return false;
   }
 }

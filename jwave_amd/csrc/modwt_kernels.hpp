@@ -48,6 +48,18 @@ __device__ __forceinline__ int64_t wrap_mod(int64_t g, int64_t N) {
   return r < 0 ? r + N : r;
 }
 
+// XCD-aware tile order.  Blocks b and b+8 share an XCD (round-robin dealing),
+// so plain order puts a tile and the neighbour whose samples form its halo on
+// different L2s: every halo is a second HBM read.  Here XCD group x = b % 8
+// walks a contiguous run of tiles, [x*q + min(x, r), ...) with q = nblk/8,
+// r = nblk%8, so neighbours run side by side on one L2.  Bijective for any
+// grid size (N is not a multiple of the tile in general).
+__device__ __forceinline__ int64_t xcd_tile() {
+  const int nblk = gridDim.x, b = blockIdx.x;
+  const int q = nblk >> 3, r = nblk & 7, x = b & 7;
+  return (int64_t)x * q + (x < r ? x : r) + (b >> 3);
+}
+
 // Forward, tiled.  src = V_{j0-1} (length N); W_j -> wout + (j-1)*ldw;
 // V_{j1} -> vout.  Grid: ceil(N/T) blocks.  LDS: (T + S) doubles.
 template <int L, int NT, int T, int SMAX, bool FMA>
@@ -59,7 +71,7 @@ __global__ __launch_bounds__(NT) void modwt_fwd_tile(const double* __restrict__ 
   constexpr int MAXP = (T + SMAX + NT - 1) / NT;
   const int nL = MB<L>::n(tp);
   const int S = (nL - 1) * ((1 << j1) - (1 << (j0 - 1)));
-  const int64_t t0 = (int64_t)blockIdx.x * T;
+  const int64_t t0 = xcd_tile() * T;
   const int tid = threadIdx.x;
   const int W = T + S;
   load_window<1, NT, MAXP>(lds, src, W, false, 0, 1,
@@ -140,7 +152,7 @@ __global__ __launch_bounds__(NT) void modwt_inv_tile(const double* __restrict__ 
   const int R = (nL - 1) * ((1 << j1) - (1 << (j0 - 1)));
   double* vb = lds;
   double* wb = lds + (T + R);
-  const int64_t t0 = (int64_t)blockIdx.x * T;
+  const int64_t t0 = xcd_tile() * T;
   const int tid = threadIdx.x;
   // W window of level j (length T + Rj) -> registers (all loads in flight)
   double pw[MAXP];
@@ -235,7 +247,7 @@ __global__ __launch_bounds__(NT) void modwt_inv_tile2(const double* __restrict__
   const int R = (nL - 1) * ((1 << j1) - (1 << (j0 - 1)));
   double* vb = lds;
   double* wb = lds + (T + R);
-  const int64_t t0 = (int64_t)blockIdx.x * T;
+  const int64_t t0 = xcd_tile() * T;
   const int tid = threadIdx.x;
   auto fetch_w = [&](double (&pw)[MAXP], int j, int W) {
     const double* wrow = coef + (int64_t)(j - 1) * ldw;
@@ -326,7 +338,7 @@ __global__ __launch_bounds__(NT) void modwt_fwd_tile_g(const double* __restrict_
   constexpr int MAXP = (T + SMAX + NT - 1) / NT;
   constexpr int NS = ModGeoG<L, NT, T, SMAX, KO>::kSlots;
   const int S = (L - 1) * ((1 << j1) - (1 << (j0 - 1)));
-  const int64_t t0 = (int64_t)blockIdx.x * T;
+  const int64_t t0 = xcd_tile() * T;
   const int tid = threadIdx.x;
   const int W = T + S;
   load_window<1, NT, MAXP>(lds, src, W, false, 0, 1,
@@ -401,7 +413,7 @@ __global__ __launch_bounds__(NT) void modwt_inv_tile_g(const double* __restrict_
   const int R = (L - 1) * ((1 << j1) - (1 << (j0 - 1)));
   double* vb = lds;
   double* wb = lds + (T + R);
-  const int64_t t0 = (int64_t)blockIdx.x * T;
+  const int64_t t0 = xcd_tile() * T;
   const int tid = threadIdx.x;
   double pw[MAXP];
   auto fetch_w = [&](int j, int W) {
