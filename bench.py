@@ -27,6 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec (an FMA counts 2 flops)
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (spec), SURVEY §8d
 
 
@@ -194,7 +195,10 @@ def setup(args, d):
                     config={"workload": "wpt: Symlet8, 6 levels, %d signals x 65536 "
                                         "(%d per GPU), forward+reverse per step" % (total, b),
                             "math": args.math, "parallelism": "batch shards x%d" % d.world},
-                    scaling="strong", cpu=None)
+                    scaling="strong", cpu=None,
+                    # 6 levels x (L = 16 taps x 2 filters) MACs per pair = 2 x 16 x 2
+                    # flops per sample per level: FP64-bound too
+                    flops_per_sample=6 * 2 * 16 * 2 / 2)
     # modwt
     n, J = 10_000_000, 8
     w = d.broadcast_taps("Daubechies4")
@@ -320,6 +324,18 @@ def main():
             "launches": ks["launches"]}
     if tsrc:
         roof["traffic_source"] = tsrc
+    if W.get("flops_per_sample"):
+        # second bound: algorithmic FP64 flops of the
+        # dominant launch over its time; EXACT mode issues mul and add
+        # separately, so its ceiling is half the FMA-counted peak
+        fl = W["flops_per_sample"] * bytes_per_launch / 16.0
+        tf = fl / (avg_ms * 1e-3) / 1e12
+        out_fp64 = {"bound": "fp64", "achieved": round(tf, 2), "peak": FP64_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(tf / FP64_PEAK_TFLOPS, 4),
+                    "flops_per_launch": fl,
+                    "exact_mode_ceiling": FP64_PEAK_TFLOPS / 2 if args.math == "exact" else None}
+    else:
+        out_fp64 = None
     kernels = {k: {"launches": v["launches"], "avg_us": round(v["total_ms"] * 1e3 / v["launches"], 2),
                    "GBps": round(v["bytes"] / (v["total_ms"] * 1e-3) / 1e9, 1)}
                for k, v in pre.items()}
@@ -332,6 +348,8 @@ def main():
            "config": W["config"], "hbm_gbps": round(gbps, 1), "roofline": roof,
            "kernels_profiled_pass": kernels, "roundtrip_max_abs_err": err,
            "ms_per_step_with_events": round(d.max(tb1 - tb0) / args.steps * 1e3, 4)}
+    if out_fp64:
+        out["roofline_fp64"] = out_fp64
     if d.rank == 0 and world == 1 and W["cpu"] and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(W["cpu"], args.cpu_seconds)
     else:
