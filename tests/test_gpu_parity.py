@@ -198,6 +198,79 @@ def test_fwt2d(ctx, wname, shape):
                      oracle.transform_2d("fwt", False, w, yr, lm, ln), "2d rev")
 
 
+@pytest.mark.parametrize("wname", ["Daubechies4", "Daubechies8"])
+@pytest.mark.parametrize("shape", [(64, 8192), (128, 4096), (64, 4096), (256, 16384)])
+def test_fwt2d_rowcap(ctx, ctx_fma, wname, shape):
+    """The row pass of >= 64 rows longer than 2048 samples (capi.cpp fwt_res_cap):
+    fwt_fwd_tile1 passes down to a 2048-sample resident tail forward, the fwt1
+    tiled reverse above a short resident head.  Config 3 takes this branch.
+    Full and partial levels; EXACT bit-exact, FMA within 1e-12*max|c|."""
+    w = jw.by_class(wname)
+    r, c = shape
+    x = rnd(r * c, r ^ c).reshape(r, c)
+    fm, fn = r.bit_length() - 1, c.bit_length() - 1
+    for lm, ln in ((fm, fn), (2, fn - 1), (fm, 3), (0, fn)):
+        yr = oracle.transform_2d("fwt", True, w, x, lm, ln)
+        assert_exact(T.transform_2d(x, w, lm, ln, True, ctx), yr,
+                     "2d fwd %s %s l=(%d,%d)" % (wname, shape, lm, ln))
+        xr = oracle.transform_2d("fwt", False, w, yr, lm, ln)
+        assert_exact(T.transform_2d(yr, w, lm, ln, False, ctx), xr,
+                     "2d rev %s %s l=(%d,%d)" % (wname, shape, lm, ln))
+        if (lm, ln) == (fm, fn):
+            assert_close(T.transform_2d(x, w, lm, ln, True, ctx_fma), yr, "2d fwd fma")
+            assert_close(T.transform_2d(yr, w, lm, ln, False, ctx_fma), xr, "2d rev fma")
+
+
+@pytest.mark.parametrize("wname", ["Haar1", "Daubechies4", "Daubechies8", "Symlet8"])
+def test_fwt_batch_rowcap(ctx, wname):
+    """Batched 1-D FWT, 64 signals x 8192 (>= 64 rows, > 2048 samples: the
+    row-cap branch), and 100 x 4096 (not a multiple of 8 rows), all levels
+    the planner treats differently."""
+    w = jw.by_class(wname)
+    for b, n in ((64, 8192), (100, 4096)):
+        x = rnd(b * n, b + n).reshape(b, n)
+        full = n.bit_length() - 1
+        for lev in (1, 2, 6, 9, full - 1, full):
+            yr = oracle.batch("fwt", True, w, x, lev)
+            assert_exact(T.fwt_forward(x, w, lev, ctx), yr, "batch fwd %d x %d l=%d" % (b, n, lev))
+            assert_exact(T.fwt_reverse(yr, w, lev, ctx), oracle.batch("fwt", False, w, yr, lev),
+                         "batch rev %d x %d l=%d" % (b, n, lev))
+
+
+@pytest.mark.parametrize("wname", ["Daubechies4", "Daubechies8"])
+def test_3d_long_lines(ctx, wname):
+    """3-D block whose innermost lines exceed 2048 samples with >= 64 of them
+    (the row-cap branch inside the slice 2-D pass), plus strided axes."""
+    w = jw.by_class(wname)
+    shape = (4, 16, 4096)
+    p, q, r = shape
+    x = rnd(p * q * r, 23).reshape(shape)
+    for lp, lq, lr in ((4, 12, 2), (2, 9, 1)):
+        yr = oracle.transform_3d("fwt", True, w, x, lp, lq, lr)
+        assert_exact(T.transform_3d(x, w, lp, lq, lr, True, ctx), yr, "3d fwd")
+        assert_exact(T.transform_3d(yr, w, lp, lq, lr, False, ctx),
+                     oracle.transform_3d("fwt", False, w, yr, lp, lq, lr), "3d rev")
+
+
+def test_fwt2d_config3_full_size(ctx, ctx_fma):
+    """Config 3 at full size: Daubechies8, 8192 x 8192, levels 13 x 13
+    (BasicTransform.java:361-474), both directions bit-exact vs the oracle in
+    EXACT mode and within 1e-12*max|c| in FMA mode; round trip vs the input."""
+    w = jw.by_class("Daubechies8")
+    n = 8192
+    x = rnd(n * n, 42).reshape(n, n)
+    yr = oracle.transform_2d("fwt", True, w, x, 13, 13)
+    y = T.transform_2d(x, w, 13, 13, True, ctx)
+    assert_exact(y, yr, "config 3 fwd")
+    assert_close(T.transform_2d(x, w, 13, 13, True, ctx_fma), yr, "config 3 fwd fma")
+    del y
+    xr = oracle.transform_2d("fwt", False, w, yr, 13, 13)
+    got = T.transform_2d(yr, w, 13, 13, False, ctx)
+    assert_exact(got, xr, "config 3 rev")
+    assert_close(T.transform_2d(yr, w, 13, 13, False, ctx_fma), xr, "config 3 rev fma")
+    assert np.abs(got - x).max() < 1e-10
+
+
 @pytest.mark.parametrize("wname", ["Haar1", "Daubechies4", "Symlet8"])
 def test_wpt2d(ctx, wname):
     w = jw.by_class(wname)
