@@ -84,16 +84,22 @@ int jwv_ctx_set_math(jwv_ctx* ctx, int mode);
 /* Pass plan for single long 1-D FWT signals (no reference counterpart; the
  * results are bit-identical under every plan).  0 = the multi-launch plan.
  * JWV_PLAN_REV_HEAD: the reverse's resident part and first tiled pass in one
- * launch; JWV_PLAN_CHAIN_REV / _FWD: the whole reverse / forward in one launch.
+ * launch (no inter-workgroup wait: every block recomputes the resident part);
+ * JWV_PLAN_CHAIN_REV / _FWD: the whole reverse / forward in one launch (the
+ * reverse chain has bounded in-kernel waits, see jwv_ctx_synchronize).
  * Default: JWV_PLAN_REV_HEAD (env JWV_PLAN overrides the default flags). */
 #define JWV_PLAN_CHAIN_REV 1
 #define JWV_PLAN_CHAIN_FWD 2
 #define JWV_PLAN_REV_HEAD 4
 int jwv_ctx_set_plan(jwv_ctx* ctx, int flags);
 /* Waits for the context's stream.  Also reports (JWV_ERR_DEVICE) a chained
- * launch whose bounded in-kernel wait gave up since the last call (its results
- * are then invalid; only possible if its grid was not co-resident). */
+ * launch whose bounded in-kernel wait gave up since the last check (its results
+ * are then invalid; only possible if its grid was not co-resident).  The
+ * host-pointer entry points make the same check before they return. */
 int jwv_ctx_synchronize(jwv_ctx* ctx);
+/* Diagnostic: bound of each in-kernel wait in polls (0 = default 2^22).  A
+ * tiny bound forces the timeout path (tests of the error contract). */
+int jwv_ctx_set_poll_limit(jwv_ctx* ctx, unsigned spins);
 /* Profiling: when enabled, every kernel launch is bracketed by a pair of
  * hipEvents recorded on the launch stream.  profile_read synchronises, sums the
  * event times per kernel kind (fwt_fwd_tile, fwt_rev_res, ...), clears the

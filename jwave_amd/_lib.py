@@ -61,6 +61,7 @@ _SIGS = {
     "jwv_ctx_set_math": [_CTX, _int],
     "jwv_ctx_set_plan": [_CTX, _int],
     "jwv_ctx_synchronize": [_CTX],
+    "jwv_ctx_set_poll_limit": [_CTX, ctypes.c_uint],
     "jwv_ctx_trim": [_CTX],
     "jwv_ctx_profile_enable": [_CTX, _int],
     "jwv_ctx_profile_select": [_CTX, ctypes.c_char_p],

@@ -57,6 +57,8 @@ struct jwv_ctx {
   // reverse ticket/flags; zeroed once, left zero by every completed launch
   unsigned* sync = nullptr;
   unsigned epoch = 0;  // reverse flag value of the last call (never 0)
+  unsigned poll_limit = 1u << 22;  // bound of every in-kernel wait (chained reverse)
+  bool waited = false;  // a launch with an in-kernel wait is queued, timeout word unchecked
   int plan = -1;       // JWV_PLAN_* bits; -1 = env defaults
   // profiling: hipEvent pairs around every kernel launch on the launch stream
   bool prof = false;
@@ -294,7 +296,8 @@ bool try_rev_chain(jwv_ctx* c, const Bank& b, const Axis& a, int h0) {
   double* wsM = grow(c, c->ws[1], (size_t)hM);
   if (++c->epoch == 0) c->epoch = 1;
   jwv::ChainRevArgs ca{a.src, a.dst, wsR, wsM, sync_words(c) + ChainGeo::kWords, (int)h, h0, nR,
-                       c->epoch};
+                       c->epoch, c->poll_limit};
+  c->waited = true;
   { ProfScope ps_(c, K_FWT_REV_CHAIN, 16.0 * h);
     hipchk(jwv::launch_fwt_rev_chain(b, use_fma(c), ca, c->stream), "fwt_rev_chain"); }
   return true;
@@ -348,7 +351,7 @@ void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
     double* ad = last ? a.dst : c->ws[pp].p;
     const AxisView av = last ? a.dv : cview(h >> K, a.inner);
     jwv::TileArgs t{cur, cv, nullptr, {}, a.dst, a.dv, ad, av, h, K, a.outer, a.inner,
-                    dma_view(cur, cv, C, a.inner)};
+                    dma_view(cur, cv, C, a.inner), h == a.len ? Geo::store_pol() : 0};
     { ProfScope ps_(c, h == a.len ? K_FWT_FWD_TILE : K_FWT_FWD_TILE_DEEP,
                     16.0 * a.outer * h * a.inner);
     hipchk(jwv::launch_fwt_fwd_tile(b, use_fma(c), C, t, c->stream), "fwt_fwd_tile"); }
@@ -406,9 +409,7 @@ void fwt_rev_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
     const int hM = cap << ChainGeo::kKM;
     const bool last = hM == a.len;
     double* out = last ? a.dst : c->ws[1].p;
-    if (++c->epoch == 0) c->epoch = 1;
-    jwv::RevHeadArgs ra{a.src, out, c->ws[0].p, sync_words(c) + ChainGeo::kWords, h,
-                        exponent(cap / h) + 1, c->epoch};
+    jwv::RevHeadArgs ra{a.src, out, h, exponent(cap / h) + 1};
     { ProfScope ps_(c, K_FWT_REV_HEAD, 16.0 * hM);
       hipchk(jwv::launch_fwt_rev_head(b, use_fma(c), ra, c->stream), "fwt_rev_head"); }
     if (last) return;
@@ -442,7 +443,8 @@ void fwt_rev_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
     double* out = last ? a.dst : c->ws[pp].p;
     const AxisView ov = last ? a.dv : cview(hK, a.inner);
     jwv::TileArgs t{acur, acv, a.src, a.sv, out, ov, nullptr, {}, h1, K, a.outer, a.inner,
-                    dma_view(acur, acv, C, a.inner) && dma_view(a.src, a.sv, C, a.inner)};
+                    dma_view(acur, acv, C, a.inner) && dma_view(a.src, a.sv, C, a.inner),
+                    last ? Geo::store_pol() : 0};
     { ProfScope ps_(c, last ? K_FWT_REV_TILE : K_FWT_REV_TILE_DEEP, 16.0 * a.outer * hK * a.inner);
     hipchk(jwv::launch_fwt_rev_tile(b, use_fma(c), C, t, c->stream), "fwt_rev_tile"); }
     acur = out;
@@ -617,6 +619,22 @@ int guarded(jwv_ctx* c, F&& f) {
   }
 }
 
+// After the stream has drained: a launch whose bounded in-kernel wait gave up
+// (fwt_rev_chain1, only if its grid was not co-resident) left its timeout word
+// set; its results are invalid -> JWV_ERR_DEVICE (JWaveError), word cleared.
+void check_waits(jwv_ctx* c) {
+  if (!c->waited || !c->sync) return;
+  c->waited = false;
+  unsigned* tmo = c->sync + ChainGeo::kWords;
+  unsigned v = 0;
+  hipchk(hipMemcpy(&v, tmo, sizeof(v), hipMemcpyDeviceToHost), "timeout word");
+  if (v) {
+    hipchk(hipMemset(tmo, 0, sizeof(v)), "timeout word");
+    throw Fail{JWV_ERR_DEVICE, "chained reverse FWT: an in-kernel wait timed out (grid not "
+                               "co-resident?); results of that call are invalid"};
+  }
+}
+
 // Host-pointer wrapper: stage in / run device body / stage out, synchronous.
 template <typename Body>
 void staged(jwv_ctx* c, const double* x, size_t nx, double* y, size_t ny, Body&& body) {
@@ -626,6 +644,7 @@ void staged(jwv_ctx* c, const double* x, size_t nx, double* y, size_t ny, Body&&
   body(dx, dy);
   hipchk(hipMemcpyAsync(y, dy, ny * sizeof(double), hipMemcpyDeviceToHost, c->stream), "D2H");
   hipchk(hipStreamSynchronize(c->stream), "sync");
+  check_waits(c);
 }
 
 // ----------------------------------------------------------------- bodies
@@ -785,7 +804,26 @@ void body_modwt_inv(jwv_ctx* c, const Bank& b, const double* wv, double* x, int6
   }
 }
 
-void need_device_ptrs(const double* x, const double* y) { check_ptrs(x, y); }
+// A _dev entry's pointers must be device memory of the context's device: a
+// kernel launched on device N must never be handed device M's buffers (nor
+// host memory).
+void check_dev_ptr(jwv_ctx* c, const void* p) {
+  hipPointerAttribute_t at{};
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();
+    throw Fail{JWV_ERR_BAD_CALL, "_dev entry point: not a HIP device pointer"};
+  }
+  if (at.type != hipMemoryTypeDevice && at.type != hipMemoryTypeManaged)
+    throw Fail{JWV_ERR_BAD_CALL, "_dev entry point given a host pointer"};
+  if (at.device != c->device)
+    throw Fail{JWV_ERR_BAD_CALL, "device pointer belongs to device " + std::to_string(at.device) +
+                                     ", the context to device " + std::to_string(c->device)};
+}
+void need_device_ptrs(jwv_ctx* c, const double* x, const double* y) {
+  check_ptrs(x, y);
+  check_dev_ptr(c, x);
+  check_dev_ptr(c, y);
+}
 
 }  // namespace
 
@@ -814,6 +852,10 @@ int Geo::stream_blocks_per_cu() {
 bool Geo::fwt1() {
   static const bool p = env_int("JWV_FWT1", 1) != 0;
   return p;
+}
+int Geo::store_pol() {
+  static const int p = env_int("JWV_STPOL", 0);
+  return p < 0 || p > 2 ? 0 : p;
 }
 bool Geo::fwt8() {
   static const bool p = env_int("JWV_FWT8", 1) != 0;
@@ -982,17 +1024,15 @@ int jwv_ctx_set_plan(jwv_ctx* c, int flags) {
 int jwv_ctx_synchronize(jwv_ctx* c) {
   return guarded(c, [&] {
     hipchk(hipStreamSynchronize(c->stream), "sync");
-    if (c->sync) {  // reverse chain timeout word (fwt1_chain.hpp)
-      unsigned* tmo = c->sync + ChainGeo::kWords;
-      unsigned v = 0;
-      hipchk(hipMemcpy(&v, tmo, sizeof(v), hipMemcpyDeviceToHost), "sync word");
-      if (v) {
-        hipchk(hipMemset(tmo, 0, sizeof(v)), "sync word");
-        throw Fail{JWV_ERR_DEVICE, "chained reverse FWT: an in-kernel wait timed out (grid not "
-                                   "co-resident?); results of that call are invalid"};
-      }
-    }
+    check_waits(c);
   });
+}
+
+int jwv_ctx_set_poll_limit(jwv_ctx* c, unsigned spins) {
+  if (!c) return set_err(nullptr, JWV_ERR_BAD_CALL, "jwv_ctx is NULL");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->poll_limit = spins ? spins : (1u << 22);
+  return JWV_OK;
 }
 
 int jwv_ctx_profile_enable(jwv_ctx* c, int on) {
@@ -1068,7 +1108,7 @@ int jwv_ctx_trim(jwv_ctx* c) {
     return guarded(c, [&] {                                                                    \
       const Bank b = make_bank(t);                                                             \
       check_1d(KIND, FWD, n, level);                                                           \
-      need_device_ptrs(x, y);                                                                  \
+      need_device_ptrs(c, x, y);                                                                  \
       check_overlap(x, (size_t)n, y, (size_t)n);                                               \
       body_1d(c, KIND, FWD, b, x, y, 1, n, n, level);                                          \
     });                                                                                        \
@@ -1100,7 +1140,7 @@ JWV_1D(jwv_wpt_rev_f64, Kind::WPT, false)
       if (batch < 0 || ld < n) throw Fail{JWV_ERR_BAD_CALL, "batch < 0 or ld < n"};             \
       check_1d(KIND, FWD, n, level);                                                            \
       if (batch == 0) return;                                                                   \
-      need_device_ptrs(x, y);                                                                   \
+      need_device_ptrs(c, x, y);                                                                   \
       const size_t tot = (size_t)((batch - 1) * ld + n);                                        \
       check_overlap(x, tot, y, tot);                                                            \
       body_1d(c, KIND, FWD, b, x, y, batch, n, ld, level);                                      \
@@ -1142,7 +1182,7 @@ static void check_2d(Kind k, bool fwd, int64_t rows, int64_t cols, int lvl_m, in
       const Bank b = make_bank(t);                                                               \
       check_2d(KIND, FWD, rows, cols, lvl_m, lvl_n);                                             \
       if (rows == 0 || cols == 0) return;                                                        \
-      need_device_ptrs(x, y);                                                                    \
+      need_device_ptrs(c, x, y);                                                                    \
       check_overlap(x, (size_t)(rows * cols), y, (size_t)(rows * cols));                         \
       body_2d(c, KIND, FWD, b, x, y, rows, cols, lvl_m, lvl_n);                                  \
     });                                                                                          \
@@ -1159,7 +1199,7 @@ static void check_2d(Kind k, bool fwd, int64_t rows, int64_t cols, int lvl_m, in
       check_1d(KIND, FWD, len, level);                                                           \
       if (outer == 0 || len == 0 || inner == 0) return;                                          \
       if (inner > (int64_t(1) << 30)) throw Fail{JWV_ERR_BAD_CALL, "inner dimension too large"}; \
-      need_device_ptrs(x, y);                                                                    \
+      need_device_ptrs(c, x, y);                                                                    \
       const size_t tot = (size_t)(outer * len * inner);                                          \
       check_overlap(x, tot, y, tot);                                                             \
       const AxisView v = cview(len, inner);                                                      \
@@ -1205,6 +1245,7 @@ static void check_3d(Kind k, bool fwd, int64_t P, int64_t Q, int64_t R, int lp, 
       check_ptrs(x, y);                                                                           \
       const size_t tot = (size_t)(P * Q * R);                                                     \
       if (DEV) {                                                                                  \
+        need_device_ptrs(c, x, y);                                                                \
         check_overlap(x, tot, y, tot);                                                            \
         body_3d(c, KIND, FWD, b, x, y, P, Q, R, lp, lq, lr);                                      \
       } else {                                                                                    \
@@ -1275,7 +1316,7 @@ int jwv_compress_magnitude_f64_dev(const double* x, double* y, int64_t n, double
   return guarded(c, [&] {
     if (n < 0) throw Fail{JWV_ERR_BAD_CALL, "n < 0"};
     if (n == 0) return;
-    need_device_ptrs(x, y);
+    need_device_ptrs(c, x, y);
     body_compress(c, x, y, n, threshold, magnitude);
   });
 }
@@ -1296,7 +1337,7 @@ int jwv_fwt_denoise_f64_dev(const double* x, double* y, int64_t n, int level, do
     const Bank b = make_bank(t);
     check_1d(Kind::FWT, true, n, level);
     if (n == 0) return;
-    need_device_ptrs(x, y);
+    need_device_ptrs(c, x, y);
     body_denoise(c, b, x, y, n, level, threshold);
   });
 }
@@ -1330,7 +1371,7 @@ int jwv_modwt_fwd_f64_dev(const double* x, double* wv, int64_t n, int J, const j
     const Bank b = make_bank(t);
     check_modwt(n, J);
     if (n == 0) return;
-    need_device_ptrs(x, wv);
+    need_device_ptrs(c, x, wv);
     check_overlap(x, (size_t)n, wv, (size_t)n * (J + 1));
     body_modwt_fwd(c, b, x, wv, n, J);
   });
@@ -1353,7 +1394,7 @@ int jwv_modwt_inv_f64_dev(const double* wv, double* x, int64_t n, int J, const j
     const Bank b = make_bank(t);
     if (J < 1 || n == 0) return;
     if (J > 13 || n > 0x7fffffffLL) throw Fail{JWV_ERR_BAD_CALL, "J > 13 or n too large"};
-    need_device_ptrs(wv, x);
+    need_device_ptrs(c, wv, x);
     check_overlap(wv, (size_t)n * (J + 1), x, (size_t)n);
     body_modwt_inv(c, b, wv, x, n, J);
   });

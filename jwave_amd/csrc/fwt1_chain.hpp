@@ -190,14 +190,14 @@ __device__ __forceinline__ void rev1_load_approx(double* lds, const double* asrc
 // Persistent grid of G co-resident blocks (G >= 1 + nM, sized by the host
 // from the occupancy query): block 0 runs R, blocks 1..nM run the M units,
 // then every block takes A tiles b, b + G, ...  ctl: [0] timeout word (set
-// by a wait that gave up; read and cleared by jwv_ctx_synchronize), [1] R
+// by a wait that gave up; read and cleared by the host after the call), [1] R
 // flag, [2 + u] M flags.  Waits are bounded (poll_eq/poll_all).
 template <int L, int NT, int CAPR, int TM, int KM, int TA, int KA, bool FMA, int MINW>
 __global__ __launch_bounds__(NT, MINW) void fwt_rev_chain1(const double* __restrict__ coef,
                                                            double* __restrict__ dst, double* wsR,
                                                            double* wsM, unsigned* ctlg, int h,
                                                            int h0R, int nR, unsigned epoch,
-                                                           RevTaps<L> tp) {
+                                                           unsigned spins, RevTaps<L> tp) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int tid = threadIdx.x, b = blockIdx.x, G = gridDim.x;
   const int hR = h0R << (nR - 1), hM = hR << KM;
@@ -218,7 +218,7 @@ __global__ __launch_bounds__(NT, MINW) void fwt_rev_chain1(const double* __restr
   } else if (b <= nM) {  // ---- M: unit u, KM levels from wsR
     const int u = b - 1;
     rev1_load_details<L, NT, TM, KM>(lds, coef, hM, u);
-    if (tid == 0) poll_eq(rflag, epoch, tmo);
+    if (tid == 0) poll_eq(rflag, epoch, tmo, spins);
     __syncthreads();
     rev1_load_approx<L, NT, TM, KM>(lds, wsR, hM, u);
     dma_fence_barrier();  // the detail DMA and the approximation window
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(NT, MINW) void fwt_rev_chain1(const double* __restr
   if (t >= nA) return;
   if (b > nM) rev1_load_details<L, NT, TA, KA>(lds, coef, h, t);
   else __syncthreads();  // R / M role done with LDS
-  if (tid < 64) poll_all(mflag, nM, epoch, tmo);
+  if (tid < 64) poll_all(mflag, nM, epoch, tmo, spins);
   __syncthreads();
   for (bool first = b > nM;; first = false) {
     if (!first) rev1_load_details<L, NT, TA, KA>(lds, coef, h, t);
@@ -291,36 +291,44 @@ __global__ __launch_bounds__(NT) void fwt_fwd_tail1(const double* __restrict__ s
   fwd_res1_levels<L, NT, CAPC, FMA>(lds, dst, hC, levC, tp);
 }
 
-// Reverse head: block 0 = R (resident synthesis of the coefficient prefix up
-// to hR, written through to wsR, then a flag), blocks 1..nM = M units (KM
-// levels from wsR + details; plain stores to wsM, read by the next launch).
-// Grid 1 + nM blocks, all co-resident (nM <= CUs); waits bounded.
-// ctl: [0] timeout word, [1] R flag (epoch of the call).
+// Reverse head: the resident deep levels (R) and the first tiled pass (M
+// units) in one launch with NO inter-workgroup dependency.  Every block is an
+// M unit that synthesises the coefficient prefix [0, hR) itself (R, resident
+// in its own LDS region: 8 KB of L2-served reads and ~10 latency-bound levels
+// per block, overlapped with its detail-window DMA), takes its level-K
+// approximation window from that LDS copy, and runs KM levels; the hR << KM
+// outputs go to wsM (plain stores, read by the next launch).  The R result is
+// identical in every block (same code, same inputs), so the output equals the
+// one-producer hand-off it replaces, without a flag, a poll or a timeout path.
+// Grid hM / TM blocks.
+template <int L, int TM, int KM>
+struct RevHeadGeo {
+  using G = Rev1Geo<L, TM, KM>;
+  static constexpr int roff() { return (G::lds_doubles() + 1) & ~1; }  // R region (16-B aligned)
+  __host__ __device__ static int lds_doubles(int hR) { return roff() + hR + 2; }
+};
+
 template <int L, int NT, int CAPR, int TM, int KM, bool FMA>
 __global__ __launch_bounds__(NT) void fwt_rev_head1(const double* __restrict__ coef,
-                                                    double* __restrict__ wsM, double* wsR,
-                                                    unsigned* ctlg, int h0R, int nR,
-                                                    unsigned epoch, RevTaps<L> tp) {
+                                                    double* __restrict__ wsM, int h0R, int nR,
+                                                    RevTaps<L> tp) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  const int tid = threadIdx.x, b = blockIdx.x;
+  using G = Rev1Geo<L, TM, KM>;
+  const int tid = threadIdx.x, u = blockIdx.x;
   const int hR = h0R << (nR - 1), hM = hR << KM;
-  if (b == 0) {
-    load_window<1, NT, (CAPR + NT - 1) / NT>(lds, coef, hR, true, 0, 1,
-                                              [&](int e) { return (int64_t)e; });
-    dma_fence_barrier();
-    rev_res1_levels<L, NT, CAPR, FMA>(lds, h0R, nR, tp);
-    for (int q = 2 * tid; q < hR; q += 2 * NT) st2<true>(wsR + q, lds[q], lds[q + 1]);
-    drain_stores();
-    __syncthreads();
-    if (tid == 0) store_agent(ctlg + 1, epoch);
-    return;
-  }
-  const int u = b - 1;
+  double* rl = lds + RevHeadGeo<L, TM, KM>::roff();
+  // one DMA burst: this unit's detail windows and the coefficient prefix
   rev1_load_details<L, NT, TM, KM>(lds, coef, hM, u);
-  if (tid == 0) poll_eq(ctlg + 1, epoch, ctlg);
-  __syncthreads();
-  rev1_load_approx<L, NT, TM, KM>(lds, wsR, hM, u);
+  load_window<1, NT, (CAPR + NT - 1) / NT>(rl, coef, hR, true, 0, 1,
+                                            [&](int e) { return (int64_t)e; });
   dma_fence_barrier();
+  rev_res1_levels<L, NT, CAPR, FMA>(rl, h0R, nR, tp);  // ends with a block barrier
+  {
+    const int BK = (u * TM >> KM) - G::c(KM), am = hR - 1;
+    double* aw = lds + ((KM & 1) ? G::buf1() : G::buf0());
+    for (int e = tid; e < G::len(KM); e += NT) aw[e] = rl[(BK + e) & am];
+  }
+  lds_barrier();
   Rev1Level<L, NT, TM, KM, FMA, KM - 1>::run(tp, lds, u, wsM);
 }
 

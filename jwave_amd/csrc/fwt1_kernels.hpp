@@ -44,7 +44,7 @@ struct Fwd1Level {
   // for the details and approximations, L+2 window reads for two pairs.
   __device__ __forceinline__ static void run(const FwdTaps<L>& tp, double* lds,
                                              double* __restrict__ yd0, int hl, int t,
-                                             double* __restrict__ ya) {
+                                             double* __restrict__ ya, int sp = 0) {
     using G = Fwd1Geo<L, T, K>;
     constexpr int mo = G::m(l);      // even
     constexpr int own = T >> l;      // even
@@ -81,7 +81,7 @@ struct Fwd1Level {
         if (l == 1)
 #endif
         if (2 * r * NT < own && (2 * (r + 1) * NT <= own || p < own))
-          *reinterpret_cast<double2*>(yd + p) = make_double2(d0, d1);
+          st2_pol(yd, p, d0, d1, sp);
       }
     }
     if constexpr (l < K) {
@@ -94,7 +94,7 @@ struct Fwd1Level {
         }
       }
       lds_barrier();
-      Fwd1Level<L, NT, T, K, FMA, l + 1, WT>::run(tp, lds, yd0, hl >> 1, t, ya);
+      Fwd1Level<L, NT, T, K, FMA, l + 1, WT>::run(tp, lds, yd0, hl >> 1, t, ya, sp);
     }
   }
 };
@@ -106,7 +106,8 @@ template <int L, int NT, int T, int K, bool FMA>
 __global__ __launch_bounds__(NT) void fwt_fwd_tile1(const double* __restrict__ src,
                                                     int64_t s_src, double* __restrict__ dst,
                                                     int64_t s_dst, double* __restrict__ adst,
-                                                    int64_t s_adst, int h, FwdTaps<L> tp) {
+                                                    int64_t s_adst, int h, FwdTaps<L> tp,
+                                                    int sp) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   using G = Fwd1Geo<L, T, K>;
   constexpr int M0 = G::m(0);
@@ -121,7 +122,7 @@ __global__ __launch_bounds__(NT) void fwt_fwd_tile1(const double* __restrict__ s
   load_window<1, NT, (M0 + NT - 1) / NT>(lds, s, M0, true, 0, 1,
                                           [&](int e) { return (int64_t)((base + e) & msk); });
   dma_fence_barrier();
-  Fwd1Level<L, NT, T, K, FMA, 1>::run(tp, lds, dst + o * s_dst, h, t, adst + o * s_adst);
+  Fwd1Level<L, NT, T, K, FMA, 1>::run(tp, lds, dst + o * s_dst, h, t, adst + o * s_adst, sp);
 }
 
 // ---------------------------------------------------------------- reverse
@@ -157,7 +158,7 @@ struct Rev1Geo {
 template <int L, int NT, int T, int K, bool FMA, int l, bool WT = false>
 struct Rev1Level {
   __device__ __forceinline__ static void run(const RevTaps<L>& tp, double* lds, int t,
-                                             double* __restrict__ y) {
+                                             double* __restrict__ y, int sp = 0) {
     using G = Rev1Geo<L, T, K>;
     constexpr int Q = G::Q;
     constexpr int np = G::len(l) / 2;                    // pairs of this level's window
@@ -186,7 +187,8 @@ struct Rev1Level {
                 xo);
         }
         if constexpr (l == 0) {  // WT: handed to another workgroup of this launch
-          st2<WT>(y + (int64_t)t * T + 2 * ml, xe, xo);
+          if constexpr (WT) st2<true>(y + (int64_t)t * T + 2 * ml, xe, xo);
+          else st2_pol(y + (int64_t)t * T, 2 * ml, xe, xo, sp);
         } else {
           *reinterpret_cast<double2*>(ob + 2 * ml) = make_double2(xe, xo);
         }
@@ -194,7 +196,7 @@ struct Rev1Level {
     }
     if constexpr (l > 0) {
       lds_barrier();
-      Rev1Level<L, NT, T, K, FMA, l - 1, WT>::run(tp, lds, t, y);
+      Rev1Level<L, NT, T, K, FMA, l - 1, WT>::run(tp, lds, t, y, sp);
     }
   }
 };
@@ -206,7 +208,8 @@ template <int L, int NT, int T, int K, bool FMA>
 __global__ __launch_bounds__(NT) void fwt_rev_tile1(const double* __restrict__ asrc,
                                                     int64_t s_a, const double* __restrict__ coef,
                                                     int64_t s_c, double* __restrict__ dst,
-                                                    int64_t s_d, int hK, RevTaps<L> tp) {
+                                                    int64_t s_d, int hK, RevTaps<L> tp,
+                                                    int sp) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   using G = Rev1Geo<L, T, K>;
   constexpr int MAXU = (G::len(1) + NT - 1) / NT;
@@ -233,7 +236,7 @@ __global__ __launch_bounds__(NT) void fwt_rev_tile1(const double* __restrict__ a
                              [&](int e) { return (int64_t)half + ((B + e) & hm); });
   }
   dma_fence_barrier();
-  Rev1Level<L, NT, T, K, FMA, K - 1>::run(tp, lds, t, dst + o * s_d);
+  Rev1Level<L, NT, T, K, FMA, K - 1>::run(tp, lds, t, dst + o * s_d, sp);
 }
 
 }  // namespace jwv

@@ -232,6 +232,23 @@ __device__ __forceinline__ void st2(double* p, double a, double b) {
     *reinterpret_cast<double2*>(p) = make_double2(a, b);
   }
 }
+// Cache policy of the 16-B output stores of the full-length passes (kernel
+// argument, wave-uniform): 0 plain; 1 sc1 (write-through: the line leaves the
+// XCD L2 with the store, so the launch ends with no dirty lines to write back
+// and the next dependent launch starts without that write-back,
+// MI355X_MICROARCH.md "boundary"); 2 nt.  base must be wave-uniform (it
+// becomes the buffer descriptor); off in doubles, < 2^28.
+typedef unsigned int jwv_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st2_pol(double* base, int off, double a, double b, int sp) {
+  if (sp == 0) {
+    *reinterpret_cast<double2*>(base + off) = make_double2(a, b);
+    return;
+  }
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7ffffff0, 0x00020000);
+  const jwv_u32x4 v = __builtin_bit_cast(jwv_u32x4, make_double2(a, b));
+  if (sp == 1) __builtin_amdgcn_raw_buffer_store_b128(v, rs, off * 8, 0, 16);
+  else __builtin_amdgcn_raw_buffer_store_b128(v, rs, off * 8, 0, 2);
+}
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ unsigned atomic_add_agent(unsigned* p, unsigned v) {
   return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -275,10 +292,12 @@ __device__ __forceinline__ void block_acquire() {
   __syncthreads();
 }
 // Bounded relaxed poll of one flag (one lane).  Never spins forever: after
-// ~2^22 polls it records a timeout and gives up (results are then wrong, the
-// host reports the timeout word; the grid still drains).
-__device__ __forceinline__ void poll_eq(const unsigned* f, unsigned v, unsigned* tmo) {
-  for (unsigned i = 0; i < (1u << 22); ++i) {
+// `lim` polls (host default 2^22) it records a timeout and gives up (results
+// are then wrong; every host entry reads the timeout word and fails with
+// JWV_ERR_DEVICE; the grid still drains).
+__device__ __forceinline__ void poll_eq(const unsigned* f, unsigned v, unsigned* tmo,
+                                        unsigned lim) {
+  for (unsigned i = 0; i < lim; ++i) {
     if (load_agent(f) == v) return;
     __builtin_amdgcn_s_sleep(2);
   }
@@ -286,9 +305,10 @@ __device__ __forceinline__ void poll_eq(const unsigned* f, unsigned v, unsigned*
 }
 
 // Wave-wide bounded poll until every flag f[0, n) equals v (one wave).
-__device__ __forceinline__ void poll_all(const unsigned* f, int n, unsigned v, unsigned* tmo) {
+__device__ __forceinline__ void poll_all(const unsigned* f, int n, unsigned v, unsigned* tmo,
+                                         unsigned lim) {
   const int lane = threadIdx.x & 63;
-  for (unsigned i = 0; i < (1u << 22); ++i) {
+  for (unsigned i = 0; i < lim; ++i) {
     bool ok = true;
     for (int k = lane; k < n; k += 64) ok = ok && load_agent(f + k) == v;
     if (__all(ok)) return;

@@ -48,6 +48,7 @@ struct TileArgs {  // tiled FWT/WPT kernels
   int64_t nouter;
   int inner;
   int dma;
+  int sp = 0;  // cache policy of the full-length output stores (st2_pol), C = 1 kernels
 };
 struct ModwtArgs {
   const double* src;  // fwd: V_{j0-1}; inv: V_{j1}
@@ -88,6 +89,10 @@ struct Geo {
   // C = 8 compile-time-geometry column-slab tiles (fwt8_kernels.hpp): env
   // JWV_FWT8 (default 1)
   static bool fwt8();
+  // st2_pol policy of the passes that write the full-length output (forward:
+  // the first tile pass's details; reverse: the last tile pass): env
+  // JWV_STPOL (0 plain, 1 sc1, 2 nt)
+  static int store_pol();
   static constexpr int kFwt1T = 2048, kRev1T = 2048, kFwt1KMax = 9;
   static constexpr int kFwt1FwdTail = 512, kFwt1RevTail = 1024;
   static constexpr int kWpt1T = 4096, kWpt1KMax = 6;  // WPT tiles (wpt1_kernels.hpp)
@@ -119,14 +124,12 @@ struct ChainRevArgs {
   unsigned* ctl;              // >= 2 + nM words
   int h, h0R, nR;
   unsigned epoch;             // != 0, new per call
+  unsigned spins;             // poll bound of each in-kernel wait
 };
-struct RevHeadArgs {  // fwt_rev_head1: R + M units in one launch
+struct RevHeadArgs {  // fwt_rev_head1: R (redundant per block) + M units in one launch
   const double* coef;
   double* wsM;                // hR << kKM doubles (read by the next launch)
-  double* wsR;                // hR doubles
-  unsigned* ctl;              // 2 words: timeout, R flag
   int h0R, nR;
-  unsigned epoch;
 };
 hipError_t launch_fwt_rev_head(const Bank&, bool fma, const RevHeadArgs&, hipStream_t);
 hipError_t launch_fwt_fwd_chain(const Bank&, bool fma, const ChainFwdArgs&, hipStream_t);

@@ -64,20 +64,19 @@ hipError_t rev_l(const Bank& b, const ChainRevArgs& a, hipStream_t s) {
   RevTaps<L> tp;
   for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
   hipLaunchKernelGGL(k, dim3((unsigned)G), dim3(NT), lds, s, a.coef, a.dst, a.wsR, a.wsM, a.ctl,
-                     a.h, a.h0R, a.nR, a.epoch, tp);
+                     a.h, a.h0R, a.nR, a.epoch, a.spins, tp);
   return hipGetLastError();
 }
 template <int L>
 hipError_t head_l(const Bank& b, const RevHeadArgs& a, hipStream_t s) {
   auto k = fwt_rev_head1<L, NT, CG::kCap, CG::kTM, CG::kKM, kFMA>;
   const int hR = a.h0R << (a.nR - 1), nM = (hR << CG::kKM) / CG::kTM;
-  const size_t lds =
-      (size_t)std::max(Rev1Geo<L, CG::kTM, CG::kKM>::lds_doubles(), hR + 2) * sizeof(double);
+  if (hR > CG::kCap || nM < 1) return hipErrorInvalidValue;
+  const size_t lds = (size_t)RevHeadGeo<L, CG::kTM, CG::kKM>::lds_doubles(hR) * sizeof(double);
   if (hipError_t e = prep_c(k, lds)) return e;
   RevTaps<L> tp;
   for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
-  hipLaunchKernelGGL(k, dim3((unsigned)(1 + nM)), dim3(NT), lds, s, a.coef, a.wsM, a.wsR, a.ctl,
-                     a.h0R, a.nR, a.epoch, tp);
+  hipLaunchKernelGGL(k, dim3((unsigned)nM), dim3(NT), lds, s, a.coef, a.wsM, a.h0R, a.nR, tp);
   return hipGetLastError();
 }
 }  // namespace

@@ -39,7 +39,7 @@ hipError_t fwd1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
   for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
   const dim3 grid((unsigned)(a.nouter * (a.h / T)));
   hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.sv.s_outer, a.dst, a.dv.s_outer, a.adst,
-                     a.av.s_outer, a.h, tp);
+                     a.av.s_outer, a.h, tp, a.sp);
   return hipGetLastError();
 }
 template <int L>
@@ -68,7 +68,7 @@ hipError_t rev1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
   const int hK = a.h << (a.K - 1);
   const dim3 grid((unsigned)(a.nouter * (hK / T)));
   hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.sv.s_outer, a.coef, a.cv.s_outer, a.dst,
-                     a.dv.s_outer, hK, tp);
+                     a.dv.s_outer, hK, tp, a.sp);
   return hipGetLastError();
 }
 template <int L>

@@ -71,6 +71,11 @@ class Context:
                 "rev_head": L.JWV_PLAN_REV_HEAD}
         self._check(self._lib.jwv_ctx_set_plan(self.handle, sum(bits[f] for f in set(flags))))
 
+    def set_poll_limit(self, spins=0):
+        """Diagnostic: bound of each in-kernel wait (chained reverse plan) in
+        polls; 0 = the default.  A tiny bound forces the timeout error path."""
+        self._check(self._lib.jwv_ctx_set_poll_limit(self.handle, int(spins)))
+
     def set_stream(self, stream_handle):
         self._check(self._lib.jwv_ctx_set_stream(self.handle, stream_handle))
 
@@ -190,8 +195,18 @@ def _ptr(out, dev):
 
 
 # --------------------------------------------------------- functional layer
+def _ctx_for(ctx, x):
+    """The caller's context, else this thread's default context on x's device
+    (a cuda:N tensor runs on device N; host arrays on device 0)."""
+    if ctx is not None:
+        return ctx
+    if _is_torch(x) and x.is_cuda:
+        return default_context(x.device.index or 0)
+    return default_context()
+
+
 def _run(fn_host, fn_dev, ctx, x, out_shape, args):
-    ctx = ctx or default_context()
+    ctx = _ctx_for(ctx, x)
     px, keep, dev = _prep(x, ctx)
     out = _empty(keep, out_shape, dev)
     lib = L.lib()
@@ -281,7 +296,7 @@ def compress_magnitude(x, threshold=1.0, ctx=None):
     """CompressorMagnitude(threshold).compress(x) on the GPU -> (y, magnitude)
     (compressions/CompressorMagnitude.java:73-84; DESIGN.md: the magnitude sum
     order differs from the JVM's, so it may differ in the last bits)."""
-    ctx = ctx or default_context()
+    ctx = _ctx_for(ctx, x)
     n = int(x.shape[0])
     mag = ctypes.c_double(0.0)
     y = _run("jwv_compress_magnitude_f64", "jwv_compress_magnitude_f64_dev", ctx, x, (n,),

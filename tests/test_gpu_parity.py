@@ -128,6 +128,49 @@ def test_fwt_chain(ctx, wname, n):
         ctx.set_plan()
 
 
+def test_chain_wait_timeout_is_an_error(ctx):
+    """A bounded in-kernel wait that gives up must fail the call
+    (JWV_ERR_DEVICE -> JWaveError), never return rc = 0 with invalid data
+    (the error contract of Transform.java:83-89 / SURVEY 8b).  A poll bound of
+    one forces the timeout in the chained reverse; the default plan has no
+    inter-workgroup wait at all and stays bit-exact under the same bound."""
+    w = jw.by_class("Daubechies4")
+    n = 1 << 20
+    x = rnd(n, 5)
+    y = oracle.fwt_forward(w, x, 20)
+    xr = oracle.fwt_reverse(w, y, 20)
+    try:
+        ctx.set_poll_limit(1)
+        ctx.set_plan({"chain_rev"})
+        with pytest.raises(jw.JWaveError, match="timed out"):
+            T.fwt_reverse(y, w, 20, ctx)
+        ctx.set_plan()  # default: reverse head, no wait -> unaffected by the bound
+        assert_exact(T.fwt_reverse(y, w, 20, ctx), xr, "rev head under poll bound 1")
+    finally:
+        ctx.set_poll_limit(0)
+        ctx.set_plan()
+    ctx.set_plan({"chain_rev"})
+    try:
+        assert_exact(T.fwt_reverse(y, w, 20, ctx), xr, "chained rev after the timeout")
+    finally:
+        ctx.set_plan()
+
+
+def test_dev_entry_rejects_foreign_pointers(ctx):
+    """_dev entry points accept only device memory of the context's device."""
+    import ctypes
+    from jwave_amd import _lib as L
+    w = jw.by_class("Daubechies4")
+    t = T._TapsHolder.of(w)
+    lib = L.lib()
+    host = np.zeros(64)
+    hp = ctypes.c_void_p(host.ctypes.data)
+    rc = lib.jwv_fwt_fwd_f64_dev(hp, hp, 64, 6, t, ctx.handle)
+    assert rc == L.JWV_ERR_BAD_CALL
+    assert b"host pointer" in lib.jwv_last_error(ctx.handle) or \
+        b"not a HIP device pointer" in lib.jwv_last_error(ctx.handle)
+
+
 def test_fwt_config2_full_size(ctx):
     """Config 2: Daubechies4, N = 2^24, full depth — exact vs oracle, and the
     round trip vs the input (reported bound from the taps' precision)."""

@@ -4,6 +4,7 @@
 // Build: hipcc -O3 --offload-arch=gfx950 -ffp-contract=off -std=c++17
 // Not part of the library.
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 #include "../../jwave_amd/csrc/fwt1_kernels.hpp"
 using namespace jwv;
@@ -14,8 +15,9 @@ __global__ void copy16(const double2* __restrict__ s, double2* __restrict__ d, l
   for (; i < n2; i += st) d[i] = s[i];
 }
 
-static const int H = 1 << 24, REPS = 24, NB = 6;  // NB buffer sets rotate: 2.3 GB > MALL
-static double *xs[NB], *ys[NB], *as_[NB], *zs[NB];
+static const int H = 1 << 24, REPS = 24;
+static int NB = 6;  // NB buffer sets rotate: 6 x 512 MB > MALL (argv[1] = 1: MALL-warm)
+static double *xs[8], *ys[8], *as_[8], *zs[8];
 static double *x, *y, *a, *z;
 static int rot = 0;
 static void next() { rot = (rot + 1) % NB; x = xs[rot]; y = ys[rot]; a = as_[rot]; z = zs[rot]; }
@@ -41,7 +43,7 @@ static void fwd() {
   const size_t lds = (size_t)Fwd1Geo<8, T, K>::lds_doubles() * 8;
   hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const float us = timeit([&] {
-    hipLaunchKernelGGL(k, dim3(H / T), dim3(NT), lds, 0, x, 0, y, 0, a, 0, H, tp);
+    hipLaunchKernelGGL(k, dim3(H / T), dim3(NT), lds, 0, x, 0, y, 0, a, 0, H, tp, 0);
   });
   printf("fwd T=%5d K=%d NT=%d lds=%6zu B  %7.2f us  %6.0f GB/s (alg 16N)\n", T, K, NT, lds, us,
          16.0 * H / us / 1e3);
@@ -55,13 +57,14 @@ static void rev() {
   const size_t lds = (size_t)Rev1Geo<8, T, K>::lds_doubles() * 8;
   hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const float us = timeit([&] {
-    hipLaunchKernelGGL(k, dim3(H / T), dim3(NT), lds, 0, a, 0, y, 0, z, 0, H, tp);
+    hipLaunchKernelGGL(k, dim3(H / T), dim3(NT), lds, 0, a, 0, y, 0, z, 0, H, tp, 0);
   });
   printf("rev T=%5d K=%d NT=%d lds=%6zu B  %7.2f us  %6.0f GB/s (alg 16N)\n", T, K, NT, lds, us,
          16.0 * H / us / 1e3);
 }
 
-int main() {
+int main(int argc, char** argv) {
+  if (argc > 1) NB = atoi(argv[1]);
   for (int i = 0; i < NB; ++i) {
     hipMalloc(&xs[i], (size_t)H * 8);
     hipMalloc(&ys[i], (size_t)H * 8);
@@ -74,7 +77,7 @@ int main() {
   next();
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  for (int g : {1024, 2048, 4096, 8192}) {
+  for (int g : {1024, 2048, 4096, 8192, 32768}) {
     const float us = timeit([&] {
       hipLaunchKernelGGL(copy16, dim3(g), dim3(256), 0, 0, (const double2*)x, (double2*)z, (long)H / 2);
     });
