@@ -3,23 +3,34 @@
 
 Default workload (config 2, the metric's configuration): 1-D FWT, Daubechies4,
 N = 2^24 fp64, full depth (24 levels).  One step = forward + reverse of one
-signal resident in HBM.  With N GPUs (torch.distributed.run, one rank per GPU,
-RCCL) every rank transforms its own signal: the single-signal FWT does not
-shard ("replicas", weak scaling).  Other workloads (--workload):
+signal resident in HBM.  With N GPUs every rank transforms its own signal: the
+single-signal FWT does not shard ("replicas", weak scaling).
+Other workloads (--workload):
   fwt2d : config 3, Daubechies8 8192x8192, 13x13 levels (rows+columns), fwd+rev
   wpt   : config 4, Symlet8 6 levels, 4096 x 65536 signals sharded over ranks
           (strong scaling), fwd+rev
   modwt : config 5, Daubechies4 J=8, N = 10^7, forwardMODWT + inverseMODWT
 
+The default run also measures config 4 as a secondary object
+("batched_wpt_strong"): the 4096 signals split over the ranks, data-resident
+per-rank compute between barriers, and, separately, the time to
+gather every rank's coefficients to rank 0 over RCCL.
+
+Launch: `python bench.py --gpus N` starts its N ranks itself (a
+torch.distributed.run child; this parent process never touches the GPU), or
+runs as one rank of an external torch.distributed.run.
+
 Prints ONE JSON line (rank 0).  value = samples transformed per second over
 all ranks (forward and reverse each count N samples); hbm_gbps = algorithmic
 bytes / time.  "roofline" is for the dominant kernel, timed with hipEvents
-recorded around its launches on its own stream during the timed region.
+recorded around its launches on its own stream during a second timed region.
 """
 import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -27,58 +38,96 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec (an FMA counts 2 flops)
-FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (spec), SURVEY §8d
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec, an FMA counts 2 flops
+WORKLOADS = ["fwt1d", "fwt2d", "wpt", "modwt"]
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--workload", default="fwt1d", choices=["fwt1d", "fwt2d", "wpt", "modwt"])
+    p.add_argument("--workload", default="fwt1d", choices=WORKLOADS)
     p.add_argument("--math", default="exact", choices=["exact", "fma"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
-    return p.parse_args()
+    p.add_argument("--no-secondary", action="store_true",
+                   help="skip the config-4 strong-scaling object of the default run")
+    p.add_argument("--dry-run", action="store_true",
+                   help="launcher/timing plumbing only: gloo on CPU, a placeholder host step, "
+                        "no transform (tests)")
+    return p.parse_args(argv)
+
+
+# ------------------------------------------------------------------ launcher
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    """`--gpus N` outside torch.distributed.run: start N ranks as ONE child
+    torch.distributed.run (one process per GPU) and return its exit code.
+    This process imports nothing that initialises the GPU."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(args.gpus), "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 class Dist:
-    def __init__(self, gpus):
-        import torch
+    def __init__(self, gpus, dry):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
-        if self.world != gpus and gpus != 1:
-            raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (gpus, self.world))
-        torch.cuda.set_device(self.local)
-        self.dev = torch.device("cuda", self.local)
+        self.dry = dry
+        if self.world != gpus:
+            raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d (run `python bench.py --gpus %d` "
+                             "alone, or as one rank of torch.distributed.run --nproc-per-node %d)"
+                             % (gpus, self.world, gpus, gpus))
         self.pg = None
+        self.dev = None
+        if not dry:
+            import torch
+            torch.cuda.set_device(self.local)
+            self.dev = torch.device("cuda", self.local)
         if self.world > 1:
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group("nccl", device_id=self.dev)
+            if dry:
+                dist.init_process_group("gloo")
+            else:
+                dist.init_process_group("nccl", device_id=self.dev)
             self.pg = dist
+
+    def sync(self):
+        if not self.dry:
+            import torch
+            torch.cuda.synchronize()
 
     def barrier(self):
         if self.pg:
-            self.pg.barrier(device_ids=[self.local])
+            if self.dry:
+                self.pg.barrier()
+            else:
+                self.pg.barrier(device_ids=[self.local])
+
+    def _reduce(self, v, op):
+        if not self.pg:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64, device=self.dev if not self.dry else "cpu")
+        self.pg.all_reduce(t, op=op)
+        return float(t.item())
 
     def max(self, v):
-        if not self.pg:
-            return v
-        import torch
-        t = torch.tensor([v], dtype=torch.float64, device=self.dev)
-        self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
-        return float(t.item())
+        return self._reduce(v, self.pg.ReduceOp.MAX if self.pg else None)
 
     def sum(self, v):
-        if not self.pg:
-            return v
-        import torch
-        t = torch.tensor([v], dtype=torch.float64, device=self.dev)
-        self.pg.all_reduce(t, op=self.pg.ReduceOp.SUM)
-        return float(t.item())
+        return self._reduce(v, self.pg.ReduceOp.SUM if self.pg else None)
 
     def broadcast_taps(self, cls):
         """Rank 0 owns the filter bank; every rank receives it over RCCL
@@ -105,14 +154,31 @@ class Dist:
 
 
 # ------------------------------------------------------------------ workloads
-def setup(args, d):
-    """-> dict(step=callable, samples_per_step, bytes_per_step, desc...)."""
+def setup_dry(args, d):
+    """--dry-run: a placeholder host step (no transform, no GPU) so the
+    launcher, barriers and max-over-ranks timing can be tested on CPU."""
+    import numpy as np
+    a = np.random.default_rng(d.rank).random(1 << 16)
+    b = np.empty_like(a)
+
+    def step():
+        np.copyto(b, a)
+
+    return dict(ctx=None, step=step, check=lambda: 0.0, samples=2 * a.size, bytes=32.0 * a.size,
+                metric="dry-run (launcher test, no transform)",
+                config={"workload": "dry-run", "parallelism": "ranks x%d" % d.world},
+                scaling="weak", cpu=None)
+
+
+def setup(args, d, workload=None):
+    """-> dict(step=callable, samples, bytes per step, metric, config, cpu spec)."""
     import numpy as np
     import torch
     import jwave_amd as jw
     from jwave_amd import _lib as L
     from jwave_amd.transforms import _TapsHolder
 
+    workload = workload or args.workload
     ctx = jw.Context(d.local, args.math)
     ctx.set_stream(torch.cuda.current_stream(d.dev).cuda_stream)
     lib = L.lib()
@@ -129,7 +195,7 @@ def setup(args, d):
         if rc:
             raise RuntimeError(lib.jwv_last_error(h).decode())
 
-    if args.workload == "fwt1d":
+    if workload == "fwt1d":
         n = 1 << 24
         w = d.broadcast_taps("Daubechies4")
         t = _TapsHolder.of(w)
@@ -151,8 +217,8 @@ def setup(args, d):
                             "wavelet": "Daubechies4", "n": n, "levels": 24, "batch_per_gpu": 1,
                             "directions_per_step": 2, "math": args.math,
                             "parallelism": "replicas x%d (one signal per GPU)" % d.world},
-                    scaling="weak", cpu=("fwt", w, n, 24))
-    if args.workload == "fwt2d":
+                    scaling="weak", cpu=("fwt1d", w))
+    if workload == "fwt2d":
         r = c = 8192
         w = d.broadcast_taps("Daubechies8")
         t = _TapsHolder.of(w)
@@ -172,8 +238,8 @@ def setup(args, d):
                     config={"workload": "fwt2d: 2D FWT Daubechies8 8192x8192, 13x13 levels, "
                                         "forward+reverse per step", "math": args.math,
                             "parallelism": "replicas x%d" % d.world},
-                    scaling="weak", cpu=None)
-    if args.workload == "wpt":
+                    scaling="weak", cpu=("fwt2d", w))
+    if workload == "wpt":
         total, n = 4096, 1 << 16
         b = total // d.world
         w = d.broadcast_taps("Symlet8")
@@ -195,7 +261,7 @@ def setup(args, d):
                     config={"workload": "wpt: Symlet8, 6 levels, %d signals x 65536 "
                                         "(%d per GPU), forward+reverse per step" % (total, b),
                             "math": args.math, "parallelism": "batch shards x%d" % d.world},
-                    scaling="strong", cpu=None,
+                    scaling="strong", cpu=("wpt", w), coef=y, signals=b, n=n,
                     # 6 levels x (L = 16 taps x 2 filters) MACs per pair = 2 x 16 x 2
                     # flops per sample per level: FP64-bound too
                     flops_per_sample=6 * 2 * 16 * 2 / 2)
@@ -219,34 +285,111 @@ def setup(args, d):
                 config={"workload": "modwt: Daubechies4, J=8, N=10^7, forwardMODWT+"
                                     "inverseMODWT per step", "math": args.math,
                         "parallelism": "replicas x%d" % d.world},
-                scaling="weak", cpu=None)
+                scaling="weak", cpu=("modwt", w))
+
+
+# ------------------------------------------------------------- CPU baseline
+def _host():
+    """(threads we may use, nproc, CPU model).  On the GPU box the process's
+    CPU share is 16 threads (os.cpu_count() shows the whole machine)."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = os.cpu_count() or 1
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return max(1, min(16, avail)), os.cpu_count() or 1, model
 
 
 def cpu_baseline(spec, seconds):
-    """The oracle's restatement of the reference CPU path, single thread, on a
-    bounded sample of the same workload (JWave has no parallel 1-D FWT:
-    FastWaveletTransform.java:90-97)."""
+    """The reference's CPU path, restated by the oracle (C, -O2
+    -ffp-contract=off), timed on this host on a bounded sample of the same
+    workload:
+      fwt1d: single thread (JWave has no parallel 1-D FWT, FastWaveletTransform.java:90-97);
+      fwt2d: ParallelTransform's rows -> join -> columns split over all host
+             threads (ParallelTransform.java:70-126), the full 8192x8192 matrix;
+      wpt:   signal-level parallel batch over all host threads
+             (ParallelizationOpportunityTest.java:80-98) on a sample of the signals;
+      modwt: single-thread DIRECT including the zero taps of the upsampled
+             filters (MODWTTransform.java:677-716) on a non-power-of-2 prefix
+             (DIRECT work per sample does not depend on N)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle
-    kind, w, n, lev = spec
-    x = np.random.default_rng(42).random(n)
+    kind, w = spec
+    threads, nproc, model = _host()
+    rng = np.random.default_rng(42)
     reps, t0 = 0, time.perf_counter()
-    while True:
-        y = oracle.fwt_forward(w, x, lev)
-        oracle.fwt_reverse(w, y, lev)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds or reps >= 50:
-            break
-    return {"value": 2.0 * n * reps / el, "unit": "samples/s", "cores": 1, "kind": "port",
-            "sample": "%d x (forward+reverse) of the same Daubechies4 N=2^24 full-depth signal, "
-                      "single thread, oracle/jwave_oracle.c (-O2 -ffp-contract=off), %.1f s"
-                      % (reps, el)}
+    if kind == "fwt1d":
+        n, used = 1 << 24, 1
+        x = rng.random(n)
+        while True:
+            y = oracle.fwt_forward(w, x, 24)
+            oracle.fwt_reverse(w, y, 24)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds or reps >= 50:
+                break
+        samples = 2.0 * n * reps
+        what = ("%d x (forward+reverse) of one Daubechies4 N=2^24 full-depth signal, single "
+                "thread" % reps)
+    elif kind == "fwt2d":
+        r = c = 8192
+        used = threads
+        x = rng.random((r, c))
+        while True:
+            y = oracle.transform_2d_par("fwt", True, w, x, 13, 13, used)
+            oracle.transform_2d_par("fwt", False, w, y, 13, 13, used)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds or reps >= 5:
+                break
+        samples = 2.0 * r * c * reps
+        what = ("%d x (forward+reverse) of Daubechies8 8192x8192 13x13, ParallelTransform "
+                "rows/join/columns on %d threads" % (reps, used))
+    elif kind == "wpt":
+        nsig, n = 64, 1 << 16
+        used = threads
+        x = rng.random((nsig, n))
+        while True:
+            y = oracle.batch_par("wpt", True, w, x, 6, used)
+            oracle.batch_par("wpt", False, w, y, 6, used)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds or reps >= 50:
+                break
+        samples = 2.0 * nsig * n * reps
+        what = ("%d x (forward+reverse) of %d Symlet8 L6 signals x 65536 (sample of the 4096), "
+                "signal-level parallel on %d threads" % (reps, nsig, used))
+    else:  # modwt
+        n, J, used = 131071, 8, 1
+        x = rng.random(n)
+        while True:
+            cf = oracle.modwt_forward(w, x, J, sparse=False)
+            oracle.modwt_inverse(w, cf, sparse=False)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds or reps >= 50:
+                break
+        samples = 2.0 * n * reps
+        what = ("%d x (forwardMODWT+inverseMODWT) Daubechies4 J=8 DIRECT (zero taps included) "
+                "on N=131071 (prefix sample; per-sample work as at N=10^7), single thread" % reps)
+    return {"value": samples / el, "unit": "samples/s", "cores": used, "kind": "port",
+            "sample": "%s, oracle/jwave_oracle*.c (-O2 -ffp-contract=off), %.1f s" % (what, el),
+            "host": {"nproc": nproc, "cpu_model": model, "threads_allowed": threads}}
 
 
-def load_traffic(kernel, math):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary."""
+# --------------------------------------------------------------- roofline
+def load_traffic(workload, kernel, math):
+    """HBM bytes per launch of `kernel` in `workload` from the committed
+    rocprofv3 PMC summaries (profiles/pmc_*.json, key "workload:kernel/math");
+    None when no summary covers that workload's kernel."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
     for f in reversed(files):
@@ -254,102 +397,142 @@ def load_traffic(kernel, math):
             d = json.load(open(f))
         except Exception:
             continue
-        ent = d.get("kernels", {}).get("%s/%s" % (kernel, math))
+        ent = d.get("kernels", {}).get("%s:%s/%s" % (workload, kernel, math))
         if ent and ent.get("hbm_bytes_per_launch"):
             return float(ent["hbm_bytes_per_launch"]), os.path.relpath(f, ROOT)
     return None, None
 
 
+def timed(d, step, steps):
+    d.barrier()
+    d.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    d.sync()
+    d.barrier()
+    return time.perf_counter() - t0
+
+
+def secondary_wpt(args, d):
+    """Config 4 (Symlet8 L6, 4096 x 65536) split over the ranks: data-resident
+    per-rank compute between barriers (max over ranks), then the gather of
+    every rank's coefficients to rank 0 over RCCL, timed separately."""
+    import torch
+    W = setup(args, d, "wpt")
+    for _ in range(2):
+        W["step"]()
+    steps = max(3, min(10, args.steps // 5))
+    el = d.max(timed(d, W["step"], steps))
+    total = W["samples"] * steps * d.world
+    out = {"workload": W["config"]["workload"], "scaling": "strong", "n_gpus": d.world,
+           "value": round(total / el, 1), "unit": "samples/s",
+           "ms_per_step": round(el / steps * 1e3, 4), "steps": steps,
+           "hbm_gbps": round(W["bytes"] * steps * d.world / el / 1e9, 1),
+           "roundtrip_max_abs_err": d.max(W["check"]())}
+    y = W["coef"]
+    nbytes = y.numel() * 8
+    if d.pg:
+        import torch.distributed as dist
+        bufs = [torch.empty_like(y) for _ in range(d.world - 1)] if d.rank == 0 else None
+
+        def gather():
+            if d.rank == 0:
+                ops = [dist.P2POp(dist.irecv, bufs[r - 1], r) for r in range(1, d.world)]
+            else:
+                ops = [dist.P2POp(dist.isend, y, 0)]
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+
+        gather()  # warm the P2P channels
+        g = d.max(timed(d, gather, 1))
+        out["gather_to_rank0_ms"] = round(g * 1e3, 3)
+        out["gather_bytes"] = nbytes * (d.world - 1)
+        out["gather_GBps_into_rank0"] = round(nbytes * (d.world - 1) / g / 1e9, 1)
+    else:
+        out["gather_to_rank0_ms"] = 0.0
+    del W
+    return out
+
+
 def main():
     args = parse()
-    import torch
-    d = Dist(args.gpus)
-    W = setup(args, d)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    d = Dist(args.gpus, args.dry_run)
+    W = setup_dry(args, d) if args.dry_run else setup(args, d)
     step, ctx = W["step"], W["ctx"]
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    d.sync()
     err = W["check"]()
 
-    # which kernel kind dominates: one short profiled pass (not timed)
-    ctx.profile_select(None)
-    ctx.profile(True)
-    for _ in range(3):
-        step()
-    ctx.profile(False)
-    pre = ctx.profile_read()
-    kname = max(pre.items(), key=lambda kv: kv[1]["total_ms"])[0]
+    pre, kname = {}, None
+    if ctx is not None:
+        # which kernel kind dominates: one short profiled pass (not timed)
+        ctx.profile_select(None)
+        ctx.profile(True)
+        for _ in range(3):
+            step()
+        ctx.profile(False)
+        pre = ctx.profile_read()
+        kname = max(pre.items(), key=lambda kv: kv[1]["total_ms"])[0]
 
     # timed region A: the metric (no events)
-    d.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    d.barrier()
-    t1 = time.perf_counter()
+    el = d.max(timed(d, step, args.steps))
 
-    # timed region B: same steps, hipEvents around the dominant kernel's
-    # launches only (on its stream) -> roofline.achieved
-    ctx.profile_select(kname)
-    ctx.profile(True)
-    d.barrier()
-    torch.cuda.synchronize()
-    tb0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    d.barrier()
-    tb1 = time.perf_counter()
-    ctx.profile(False)
-    prof = ctx.profile_read()
-    ctx.profile_select(None)
+    out_roof, out_fp64, tb = None, None, None
+    if ctx is not None:
+        # timed region B: same steps, hipEvents around the dominant kernel's
+        # launches only (on its stream) -> roofline.achieved
+        ctx.profile_select(kname)
+        ctx.profile(True)
+        tb = d.max(timed(d, step, args.steps))
+        ctx.profile(False)
+        prof = ctx.profile_read()
+        ctx.profile_select(None)
+        ks = prof[kname]
+        avg_ms = ks["total_ms"] / ks["launches"]
+        bytes_per_launch = ks["bytes"] / ks["launches"]
+        achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+        traffic, tsrc = load_traffic(args.workload, kname, args.math)
+        out_roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                    "kernel": kname, "avg_launch_us": round(avg_ms * 1e3, 2),
+                    "algorithmic_bytes_per_launch": bytes_per_launch, "launches": ks["launches"]}
+        if tsrc:
+            out_roof["traffic_source"] = tsrc
+        if W.get("flops_per_sample"):
+            # second bound (SURVEY.md 8d config 4): algorithmic FP64 flops of the
+            # dominant launch over its time; EXACT mode issues mul and add
+            # separately, so its ceiling is half the FMA-counted peak
+            fl = W["flops_per_sample"] * bytes_per_launch / 16.0
+            tf = fl / (avg_ms * 1e-3) / 1e12
+            out_fp64 = {"bound": "fp64", "achieved": round(tf, 2), "peak": FP64_PEAK_TFLOPS,
+                        "unit": "TFLOP/s", "frac": round(tf / FP64_PEAK_TFLOPS, 4),
+                        "flops_per_launch": fl,
+                        "exact_mode_ceiling": FP64_PEAK_TFLOPS / 2 if args.math == "exact" else None}
 
-    el = d.max(t1 - t0)
     world = d.world
-    samples = W["samples"] * args.steps * world
-    value = samples / el
+    value = W["samples"] * args.steps * world / el
     gbps = W["bytes"] * args.steps * world / el / 1e9
-
-    ks = prof[kname]
-    avg_ms = ks["total_ms"] / ks["launches"]
-    bytes_per_launch = ks["bytes"] / ks["launches"]
-    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-    traffic, tsrc = load_traffic(kname, args.math)
-    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "kernel": kname,
-            "avg_launch_us": round(avg_ms * 1e3, 2), "algorithmic_bytes_per_launch": bytes_per_launch,
-            "launches": ks["launches"]}
-    if tsrc:
-        roof["traffic_source"] = tsrc
-    if W.get("flops_per_sample"):
-        # second bound: algorithmic FP64 flops of the
-        # dominant launch over its time; EXACT mode issues mul and add
-        # separately, so its ceiling is half the FMA-counted peak
-        fl = W["flops_per_sample"] * bytes_per_launch / 16.0
-        tf = fl / (avg_ms * 1e-3) / 1e12
-        out_fp64 = {"bound": "fp64", "achieved": round(tf, 2), "peak": FP64_PEAK_TFLOPS,
-                    "unit": "TFLOP/s", "frac": round(tf / FP64_PEAK_TFLOPS, 4),
-                    "flops_per_launch": fl,
-                    "exact_mode_ceiling": FP64_PEAK_TFLOPS / 2 if args.math == "exact" else None}
-    else:
-        out_fp64 = None
     kernels = {k: {"launches": v["launches"], "avg_us": round(v["total_ms"] * 1e3 / v["launches"], 2),
                    "GBps": round(v["bytes"] / (v["total_ms"] * 1e-3) / 1e9, 1)}
                for k, v in pre.items()}
-
     out = {"metric": W["metric"], "value": round(value, 1), "unit": "samples/s",
            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True,
-           "scaling": W["scaling"], "vs_baseline": None, "dtype": "f64",
-           "data": "synthetic (uniform [0,1) doubles, seed 42+rank)",
-           "config": W["config"], "hbm_gbps": round(gbps, 1), "roofline": roof,
-           "kernels_profiled_pass": kernels, "roundtrip_max_abs_err": err,
-           "ms_per_step_with_events": round(d.max(tb1 - tb0) / args.steps * 1e3, 4)}
+           "scaling": W["scaling"], "vs_baseline": None,
+           "dtype": "f64", "data": "synthetic (uniform [0,1) doubles, seed 42+rank)",
+           "config": W["config"], "hbm_gbps": round(gbps, 1), "roofline": out_roof,
+           "kernels_profiled_pass": kernels, "roundtrip_max_abs_err": err}
+    if tb is not None:
+        out["ms_per_step_with_events"] = round(tb / args.steps * 1e3, 4)
     if out_fp64:
         out["roofline_fp64"] = out_fp64
+    if (not args.dry_run and args.workload == "fwt1d" and not args.no_secondary):
+        out["batched_wpt_strong"] = secondary_wpt(args, d)
     if d.rank == 0 and world == 1 and W["cpu"] and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(W["cpu"], args.cpu_seconds)
     else:

@@ -184,6 +184,14 @@ struct ProfScope {
   size_t idx = 0;
   ProfScope(jwv_ctx* c_, int kind, double bytes)
       : c(c_), on(c_->prof && (c_->prof_only < 0 || c_->prof_only == kind)) {
+    // env JWV_LAUNCH_LOG=1: one stderr line per launch, in launch order, so a
+    // rocprofv3 --pmc run can attribute its dispatches to the planner's
+    // kernel kinds (tools/pmc_traffic.py)
+    static const bool log = [] {
+      const char* v = std::getenv("JWV_LAUNCH_LOG");
+      return v && *v == '1';
+    }();
+    if (log) std::fprintf(stderr, "JWV_LAUNCH %s %.0f\n", kKindNames[kind], bytes);
     if (!on) return;
     jwv_ctx::Rec r{kind, bytes, take_event(c), take_event(c)};
     hipchk(hipEventRecord(r.e0, c->stream), "hipEventRecord");
@@ -324,10 +332,14 @@ void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
   const bool f1 = fast1(b, a, false);
   // levels of the tiled pass at level-input size h: KM, except that on the
   // fwt1 path the pass that ends the tiled part runs on down to kFwt1FwdTail
+  // the first pass of one long signal may use its own tile / level count
+  const bool first1 = f1 && a.outer == 1 && a.len > cap &&
+                      (a.len >> Geo::fwd1_first_k()) > cap && a.len % Geo::fwd1_first_t() == 0;
   auto pick_k = [&](int h, int rem) {
+    if (first1 && h == a.len) return std::min(rem, Geo::fwd1_first_k());
     int K = std::min(rem, KM);
     if (f1 && (h >> K) <= cap)
-      K = std::min(rem, std::min(exponent(h) - exponent(Geo::kFwt1FwdTail), Geo::kFwt1KMax));
+      K = std::min(rem, std::min(exponent(h) - exponent(Geo::fwd1_tail()), Geo::kFwt1KMax));
     return K;
   };
   // workspace: the largest intermediate approximation
@@ -351,7 +363,9 @@ void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
     double* ad = last ? a.dst : c->ws[pp].p;
     const AxisView av = last ? a.dv : cview(h >> K, a.inner);
     jwv::TileArgs t{cur, cv, nullptr, {}, a.dst, a.dv, ad, av, h, K, a.outer, a.inner,
-                    dma_view(cur, cv, C, a.inner), h == a.len ? Geo::store_pol() : 0};
+                    dma_view(cur, cv, C, a.inner), h == a.len ? Geo::store_pol() : 0,
+                    first1 && h == a.len && Geo::fwd1_first_t() != Geo::kFwt1T
+                        ? Geo::fwd1_first_t() : 0};
     { ProfScope ps_(c, h == a.len ? K_FWT_FWD_TILE : K_FWT_FWD_TILE_DEEP,
                     16.0 * a.outer * h * a.inner);
     hipchk(jwv::launch_fwt_fwd_tile(b, use_fma(c), C, t, c->stream), "fwt_fwd_tile"); }
@@ -856,6 +870,24 @@ bool Geo::fwt1() {
 int Geo::store_pol() {
   static const int p = env_int("JWV_STPOL", 0);
   return p < 0 || p > 2 ? 0 : p;
+}
+int Geo::fwd1_first_t() {
+  static const int t = env_int("JWV_FWD1T", kFwt1T) == 1024 ? 1024 : kFwt1T;
+  return t;
+}
+int Geo::fwd1_first_k() {
+  static const int k = [] {
+    const int v = env_int("JWV_FWD1K", kFwtK1);
+    return fwd1_first_t() == 1024 ? std::max(4, std::min(6, v)) : std::max(1, std::min(kFwt1KMax, v));
+  }();
+  return k;
+}
+int Geo::fwd1_tail() {
+  static const int t = [] {
+    const int v = env_int("JWV_FWD1TAIL", kFwt1FwdTail);
+    return (v == 256 || v == 512 || v == 1024 || v == 2048) ? v : kFwt1FwdTail;
+  }();
+  return t;
 }
 bool Geo::fwt8() {
   static const bool p = env_int("JWV_FWT8", 1) != 0;

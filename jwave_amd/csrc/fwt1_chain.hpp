@@ -317,12 +317,15 @@ __global__ __launch_bounds__(NT) void fwt_rev_head1(const double* __restrict__ c
   const int tid = threadIdx.x, u = blockIdx.x;
   const int hR = h0R << (nR - 1), hM = hR << KM;
   double* rl = lds + RevHeadGeo<L, TM, KM>::roff();
+  JWV_STAMP(0);
   // one DMA burst: this unit's detail windows and the coefficient prefix
   rev1_load_details<L, NT, TM, KM>(lds, coef, hM, u);
   load_window<1, NT, (CAPR + NT - 1) / NT>(rl, coef, hR, true, 0, 1,
                                             [&](int e) { return (int64_t)e; });
   dma_fence_barrier();
+  JWV_STAMP(1);
   rev_res1_levels<L, NT, CAPR, FMA>(rl, h0R, nR, tp);  // ends with a block barrier
+  JWV_STAMP(30);
   {
     const int BK = (u * TM >> KM) - G::c(KM), am = hR - 1;
     double* aw = lds + ((KM & 1) ? G::buf1() : G::buf0());
@@ -330,6 +333,7 @@ __global__ __launch_bounds__(NT) void fwt_rev_head1(const double* __restrict__ c
   }
   lds_barrier();
   Rev1Level<L, NT, TM, KM, FMA, KM - 1>::run(tp, lds, u, wsM);
+  JWV_STAMP(31);
 }
 
 }  // namespace jwv

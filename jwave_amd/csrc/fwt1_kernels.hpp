@@ -46,6 +46,7 @@ struct Fwd1Level {
                                              double* __restrict__ yd0, int hl, int t,
                                              double* __restrict__ ya, int sp = 0) {
     using G = Fwd1Geo<L, T, K>;
+    JWV_STAMP(10 + l);
     constexpr int mo = G::m(l);      // even
     constexpr int own = T >> l;      // even
     constexpr int NP2 = mo / 2;      // pair couples
@@ -119,9 +120,11 @@ __global__ __launch_bounds__(NT) void fwt_fwd_tile1(const double* __restrict__ s
   const int64_t o = b / ntile;
   const double* s = src + o * s_src;
   const int msk = h - 1, base = t * T;
+  JWV_STAMP(0);
   load_window<1, NT, (M0 + NT - 1) / NT>(lds, s, M0, true, 0, 1,
                                           [&](int e) { return (int64_t)((base + e) & msk); });
   dma_fence_barrier();
+  JWV_STAMP(1);
   Fwd1Level<L, NT, T, K, FMA, 1>::run(tp, lds, dst + o * s_dst, h, t, adst + o * s_adst, sp);
 }
 
@@ -160,6 +163,7 @@ struct Rev1Level {
   __device__ __forceinline__ static void run(const RevTaps<L>& tp, double* lds, int t,
                                              double* __restrict__ y, int sp = 0) {
     using G = Rev1Geo<L, T, K>;
+    JWV_STAMP(20 + l);
     constexpr int Q = G::Q;
     constexpr int np = G::len(l) / 2;                    // pairs of this level's window
     constexpr int off = G::c(l + 1) - G::c(l) / 2;       // local index of a[pair 0]
@@ -174,17 +178,18 @@ struct Rev1Level {
       if ((r + 1) * NT <= np || ml < np) {
         const int li = off + ml;
         double xe, xo;
-        rev_pair<L, FMA>(tp, ab + li, db + li, 1, xe, xo);
         // array-head pairs (global pair index in [0, Q-1)): in tile 0, and in
         // the halo of the next tiles at deep levels where c_l > T/2^l.  The
-        // window's first global pair pbase decides for the whole block.
+        // window's first global pair pbase decides for the whole block; those
+        // blocks take the rotated form for every pair of the slot (one path).
         const int pbase = t * (T >> (l + 1)) - G::c(l) / 2;
         if (r == 0 && pbase < Q - 1) {
           const int mg = pbase + ml;
-          if (mg >= 0 && mg < Q - 1)
-            rev_pair_head<L, FMA>(
-                tp, mg, [=](int q) { return ab[li - q]; }, [=](int q) { return db[li - q]; }, xe,
-                xo);
+          rev_pair_rot<L, FMA>(tp, [=](int q) { return ab[li - q]; },
+                               [=](int q) { return db[li - q]; },
+                               (mg >= 0 && mg < Q - 1) ? mg : Q - 1, xe, xo);
+        } else {
+          rev_pair<L, FMA>(tp, ab + li, db + li, 1, xe, xo);
         }
         if constexpr (l == 0) {  // WT: handed to another workgroup of this launch
           if constexpr (WT) st2<true>(y + (int64_t)t * T + 2 * ml, xe, xo);

@@ -171,6 +171,43 @@ __device__ __forceinline__ void rev_pair(const typename FB<L>::Rev& tp, const do
   xo = so;
 }
 
+// Interior and array-head pairs in one branch-free form (compiled-in even L):
+// rev_pair_head's order (q = mg..0, then Q-1..mg+1) is the interior order
+// (q = Q-1..0) rotated, over the same per-term values.  r = mg for a head
+// pair (mg < Q-1), r = Q-1 for every other pair; the rotation is a register
+// select, so a wave holding both kinds of pair runs ONE path (rev_pair +
+// rev_pair_head under divergence run both, and every level of a resident
+// reverse has its head lanes in wave 0).  Results are bit-identical to
+// rev_pair / rev_pair_head.
+template <int L, bool FMA, typename GA, typename GD>
+__device__ __forceinline__ void rev_pair_rot(const RevTaps<L>& tp, GA A, GD D, int r, double& xe,
+                                             double& xo) {
+  static_assert(L >= 2 && (L & 1) == 0, "compiled-in even banks only");
+  constexpr int Q = L / 2;
+  double te[Q], to[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const double a = A(q), d = D(q);
+    te[q] = mac<FMA>(a * tp.lo_r[2 * q], d, tp.hi_r[2 * q]);
+    to[q] = mac<FMA>(a * tp.lo_r[2 * q + 1], d, tp.hi_r[2 * q + 1]);
+  }
+  double se = 0.0, so = 0.0;
+#pragma unroll
+  for (int k = 0; k < Q; ++k) {
+    const int q = (r - k) & (Q - 1);
+    double ve = te[0], vo = to[0];
+#pragma unroll
+    for (int i = 1; i < Q; ++i) {
+      ve = q == i ? te[i] : ve;
+      vo = q == i ? to[i] : vo;
+    }
+    se += ve;
+    so += vo;
+  }
+  xe = se;
+  xo = so;
+}
+
 // Levels with h < L wrap several times: emulate the scatter literally
 // (i ascending, j ascending).  Only for tiny h (h < L <= 64), per output k.
 template <int L, bool FMA>

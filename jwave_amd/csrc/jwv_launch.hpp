@@ -49,6 +49,7 @@ struct TileArgs {  // tiled FWT/WPT kernels
   int inner;
   int dma;
   int sp = 0;  // cache policy of the full-length output stores (st2_pol), C = 1 kernels
+  int t1 = 0;  // C = 1 forward tile: 0 = Geo::kFwt1T, or 1024 (first pass of a long signal)
 };
 struct ModwtArgs {
   const double* src;  // fwd: V_{j0-1}; inv: V_{j1}
@@ -93,6 +94,12 @@ struct Geo {
   // the first tile pass's details; reverse: the last tile pass): env
   // JWV_STPOL (0 plain, 1 sc1, 2 nt)
   static int store_pol();
+  // First (full-length) forward pass of one long contiguous signal: tile
+  // (2048 | 1024, env JWV_FWD1T) and fused levels (env JWV_FWD1K); the last
+  // forward tile pass runs down to fwd1_tail() samples (env JWV_FWD1TAIL).
+  static int fwd1_first_t();
+  static int fwd1_first_k();
+  static int fwd1_tail();
   static constexpr int kFwt1T = 2048, kRev1T = 2048, kFwt1KMax = 9;
   static constexpr int kFwt1FwdTail = 512, kFwt1RevTail = 1024;
   static constexpr int kWpt1T = 4096, kWpt1KMax = 6;  // WPT tiles (wpt1_kernels.hpp)

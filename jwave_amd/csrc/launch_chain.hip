@@ -69,14 +69,16 @@ hipError_t rev_l(const Bank& b, const ChainRevArgs& a, hipStream_t s) {
 }
 template <int L>
 hipError_t head_l(const Bank& b, const RevHeadArgs& a, hipStream_t s) {
-  auto k = fwt_rev_head1<L, NT, CG::kCap, CG::kTM, CG::kKM, kFMA>;
+  // 512 threads: the wide levels of R and M take half the pair slots
+  constexpr int NTH = 512;
+  auto k = fwt_rev_head1<L, NTH, CG::kCap, CG::kTM, CG::kKM, kFMA>;
   const int hR = a.h0R << (a.nR - 1), nM = (hR << CG::kKM) / CG::kTM;
   if (hR > CG::kCap || nM < 1) return hipErrorInvalidValue;
   const size_t lds = (size_t)RevHeadGeo<L, CG::kTM, CG::kKM>::lds_doubles(hR) * sizeof(double);
   if (hipError_t e = prep_c(k, lds)) return e;
   RevTaps<L> tp;
   for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
-  hipLaunchKernelGGL(k, dim3((unsigned)nM), dim3(NT), lds, s, a.coef, a.wsM, a.h0R, a.nR, tp);
+  hipLaunchKernelGGL(k, dim3((unsigned)nM), dim3(NTH), lds, s, a.coef, a.wsM, a.h0R, a.nR, tp);
   return hipGetLastError();
 }
 }  // namespace

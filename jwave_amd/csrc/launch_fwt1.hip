@@ -45,6 +45,14 @@ hipError_t fwd1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
 template <int L>
 hipError_t fwd1_l(const Bank& b, const TileArgs& a, hipStream_t s) {
   constexpr int NT = 256, T = kFwdT;
+  if (a.t1 == 1024) {  // first pass of a long signal (Geo::fwd1_first_t)
+    switch (a.K) {
+      case 4: return fwd1_k<L, NT, 1024, 4>(b, a, s);
+      case 5: return fwd1_k<L, NT, 1024, 5>(b, a, s);
+      case 6: return fwd1_k<L, NT, 1024, 6>(b, a, s);
+      default: return hipErrorInvalidValue;
+    }
+  }
   switch (a.K) {
     case 1: return fwd1_k<L, NT, T, 1>(b, a, s);
     case 2: return fwd1_k<L, NT, T, 2>(b, a, s);
@@ -52,9 +60,11 @@ hipError_t fwd1_l(const Bank& b, const TileArgs& a, hipStream_t s) {
     case 4: return fwd1_k<L, NT, T, 4>(b, a, s);
     case 5: return fwd1_k<L, NT, T, 5>(b, a, s);
     case 6: return fwd1_k<L, NT, T, 6>(b, a, s);
-    case 7: return fwd1_k<L, NT, T, 7>(b, a, s);
-    case 8: return fwd1_k<L, NT, T, 8>(b, a, s);
-    default: return fwd1_k<L, NT, T, 9>(b, a, s);
+    // deep passes (latency-bound, few blocks): 512 threads halve the pair
+    // slots of the wide levels (config 2: 0.6 us per call)
+    case 7: return fwd1_k<L, 512, T, 7>(b, a, s);
+    case 8: return fwd1_k<L, 512, T, 8>(b, a, s);
+    default: return fwd1_k<L, 512, T, 9>(b, a, s);
   }
 }
 
@@ -204,7 +214,8 @@ bool fwt_fwd_tile1(const Bank& b, const TileArgs& a, hipStream_t s, hipError_t& 
   if (((uintptr_t)a.dst & 15) || ((uintptr_t)a.adst & 15) || !even_rows(a.dv, a.nouter) ||
       !even_rows(a.av, a.nouter))
     return false;
-  if (a.h % kFwdT) return false;
+  if (a.t1 != 0 && (a.t1 != 1024 || a.K < 4 || a.K > 6)) return false;
+  if (a.h % (a.t1 ? a.t1 : kFwdT)) return false;
   switch (b.L) {
     case 2: err = fwd1_l<2>(b, a, s); return true;
     case 4: err = fwd1_l<4>(b, a, s); return true;

@@ -24,8 +24,9 @@ class _Taps(ctypes.Structure):
 
 
 def build(force=False):
-    src = os.path.join(_HERE, "jwave_oracle.c")
-    if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+    srcs = [os.path.join(_HERE, f) for f in ("jwave_oracle.c", "jwave_oracle_par.c", "Makefile")]
+    if force or not os.path.exists(_LIB_PATH) or \
+            any(os.path.getmtime(_LIB_PATH) < os.path.getmtime(s) for s in srcs):
         subprocess.check_call(["make", "-s", "-C", _HERE])
     return _LIB_PATH
 
@@ -44,6 +45,8 @@ def lib():
             getattr(_lib, name).argtypes = [c_int, tp, _dp, _dp, c_int, c_int, c_int, c_int]
         for name in ("orc_3d_forward", "orc_3d_reverse"):
             getattr(_lib, name).argtypes = [c_int, tp, _dp, _dp] + [c_int] * 6
+        _lib.orc_2d_par.argtypes = [c_int, c_int, tp, _dp, _dp] + [c_int] * 5
+        _lib.orc_batch_par.argtypes = [c_int, c_int, tp, _dp, _dp, c_int, c_int, i64, c_int, c_int]
         _lib.orc_modwt_forward.argtypes = [tp, _dp, _dp, c_int, c_int, c_int]
         _lib.orc_modwt_inverse.argtypes = [tp, _dp, _dp, c_int, c_int, c_int]
         _lib.orc_modwt_filters.argtypes = [tp, _dp, _dp]
@@ -122,6 +125,24 @@ def batch(kind, forward, wavelet, x, level):
     x = _f64(x); y = np.empty_like(x); t = OracleTaps(wavelet)
     b, n = x.shape
     _check(lib().orc_batch(_KIND[kind], int(forward), t.ref(), _ptr(x), _ptr(y), b, n, n, int(level)))
+    return y
+
+
+def batch_par(kind, forward, wavelet, x, level, nthreads):
+    """Signal-level parallel batch (ParallelizationOpportunityTest.java:80-98)."""
+    x = _f64(x); y = np.empty_like(x); t = OracleTaps(wavelet)
+    b, n = x.shape
+    _check(lib().orc_batch_par(_KIND[kind], int(forward), t.ref(), _ptr(x), _ptr(y), b, n, n,
+                               int(level), int(nthreads)))
+    return y
+
+
+def transform_2d_par(kind, forward, wavelet, x, lvl_m, lvl_n, nthreads):
+    """ParallelTransform 2-D (ParallelTransform.java:70-126): rows, join, columns."""
+    x = _f64(x); y = np.empty_like(x); t = OracleTaps(wavelet)
+    r, c = x.shape
+    _check(lib().orc_2d_par(_KIND[kind], int(forward), t.ref(), _ptr(x), _ptr(y), r, c,
+                            int(lvl_m), int(lvl_n), int(nthreads)))
     return y
 
 

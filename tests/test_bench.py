@@ -1,0 +1,59 @@
+"""bench.py plumbing on CPU: the --gpus N launcher (one child
+torch.distributed.run, gloo in --dry-run), the JSON line contract, and the
+CPU-baseline legs of every workload (bounded, host only)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _json_line(out):
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert lines, out[-2000:]
+    return json.loads(lines[-1])
+
+
+@pytest.mark.parametrize("gpus", [1, 2])
+def test_launcher_dry_run(gpus):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus),
+                        "--dry-run", "--steps", "3", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == gpus
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in d
+    assert d["value"] > 0 and d["steps"] == 3
+
+
+def test_world_mismatch_is_explained():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--dry-run"], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0
+    assert "torch.distributed.run" in (r.stderr + r.stdout)
+
+
+@pytest.mark.parametrize("kind", ["fwt1d", "wpt", "modwt"])
+def test_cpu_baseline_legs(kind):
+    import bench
+    import jwave_amd as jw
+    w = jw.by_class({"fwt1d": "Daubechies4", "wpt": "Symlet8", "modwt": "Daubechies4"}[kind])
+    cb = bench.cpu_baseline((kind, w), 0.01)
+    assert cb["value"] > 0 and cb["unit"] == "samples/s" and cb["kind"] == "port"
+    assert cb["cores"] >= 1 and cb["host"]["nproc"] >= 1 and cb["host"]["cpu_model"]
+
+
+def test_load_traffic_is_keyed_by_workload():
+    import bench
+    # no committed summary holds a "nosuch" workload: never borrow another's bytes
+    assert bench.load_traffic("nosuch", "fwt_fwd_tile", "exact") == (None, None)

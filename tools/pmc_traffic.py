@@ -1,88 +1,99 @@
 #!/usr/bin/env python3
 """Parse two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE; separate passes as
-MI355X_MICROARCH.md §rocprofv3 requires) into HBM bytes per launch per kernel.
+MI355X_MICROARCH.md §rocprofv3 requires) into HBM bytes per launch, per
+(workload, planner kernel kind, math mode).
 
-Correction (MI355X_MICROARCH.md §HBM / cdna_hip_programming.md §7): counter
-values are KB; FETCH_SIZE under-reports wide streaming reads on gfx950, and
-other access widths are uncalibrated.  We therefore calibrate both counters on
-the copy_axis kernel of the same run, whose bytes are known exactly (8 B per
-lane loads/stores like our FWT kernels): factor = known / counted.
+Attribution: the driver ran with JWV_LAUNCH_LOG=1, so the library printed one
+line per launch ("JWV_LAUNCH <kind> <algorithmic bytes>") in launch order; the
+jwv dispatches of each counter pass, in dispatch order, are paired with those
+lines one to one (the same deterministic launch sequence).  Keys therefore
+follow capi.cpp's kinds exactly (e.g. fwt_fwd_tile = every full-length tile
+pass of that workload, rows and column slabs alike), never another workload's.
 
-usage: pmc_traffic.py FETCH_DIR WRITE_DIR OUT.json [calib_bytes_each_way]
+Correction (MI355X_MICROARCH.md §HBM): counter values are KB; FETCH_SIZE
+reports half the bytes of a wide streaming read on gfx950.  Both counters are
+calibrated on the copy_axis launches of the same run, whose bytes are known
+exactly: factor = known / counted (expect 2.0 for FETCH, 1.0 for WRITE).
+
+usage: pmc_traffic.py WORKLOAD MATH FETCH_DIR FETCH_LOG WRITE_DIR WRITE_LOG OUT.json
 """
 import csv
 import glob
 import json
 import os
-import re
 import sys
 from collections import defaultdict
 
-KINDS = ["fwt_fwd_tile", "fwt_fwd_res", "fwt_rev_tile", "fwt_rev_res", "wpt_fwd_tile",
-         "wpt_fwd_res", "wpt_rev_tile", "wpt_rev_res", "modwt_fwd_tile", "modwt_fwd_level",
-         "modwt_inv_tile", "modwt_inv_level", "fwt_rev_head", "fwt_fwd_chain", "fwt_rev_chain",
-         "copy_axis_kernel"]
-# tiled FWT passes: the launch over the full-length axis keeps the kind's name,
-# passes over intermediate approximations (smaller grids) become "<kind>_deep"
-# (the split capi.cpp's profiler uses).
-DEEP_SPLIT = ("fwt_fwd_tile", "fwt_rev_tile")
+CALIB_BYTES = 8.0 * (1 << 24)  # copy_axis: 2^24 doubles each way
 
 
-def kind_of(name):
-    for k in KINDS:
-        if k in name:
-            m = re.search(r"Lb([01])E", name)
-            mode = {"0": "exact", "1": "fma"}.get(m.group(1)) if m else "exact"
-            return k.replace("_kernel", ""), mode
-    return None, None
-
-
-def read(dirpath, counter):
-    files = glob.glob(os.path.join(dirpath, "**", "*counter_collection.csv"), recursive=True)
-    vals = defaultdict(list)
-    for f in files:
-        with open(f) as fh:
-            for row in csv.DictReader(fh):
-                if row.get("Counter_Name") != counter:
-                    continue
-                k, mode = kind_of(row.get("Kernel_Name", ""))
-                if k:
-                    vals[(k, mode, int(row.get("Grid_Size") or 0))].append(float(row["Counter_Value"]))
-    out = defaultdict(list)
-    for (k, mode, grid), vs in vals.items():
-        grids = [g for (k2, m2, g) in vals if k2 == k and m2 == mode]
-        if k in DEEP_SPLIT and grid < max(grids):
-            k = k + "_deep"
-        out[(k, mode)].extend(vs)
+def launches(logfile):
+    out = []
+    for line in open(logfile, errors="replace"):
+        if line.startswith("JWV_LAUNCH "):
+            _, kind, b = line.split()[:3]
+            out.append((kind, float(b)))
     return out
 
 
+def dispatches(dirpath, counter):
+    files = glob.glob(os.path.join(dirpath, "**", "*counter_collection.csv"), recursive=True)
+    rows = {}
+    for f in files:
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                if r.get("Counter_Name") != counter or "jwv::" not in r.get("Kernel_Name", ""):
+                    continue
+                key = int(r.get("Dispatch_Id") or r.get("Correlation_Id") or 0)
+                name = r["Kernel_Name"].split("(")[0].replace("void ", "")
+                ent = rows.setdefault(key, [name, 0.0])
+                ent[1] += float(r["Counter_Value"])  # summed over XCD/instance rows
+    return [rows[k] for k in sorted(rows)]
+
+
+def attribute(dirpath, counter, logfile):
+    disp = dispatches(dirpath, counter)
+    lau = launches(logfile)
+    if len(disp) != len(lau):
+        raise SystemExit("%s: %d jwv dispatches vs %d logged launches" % (counter, len(disp), len(lau)))
+    per = defaultdict(lambda: {"kb": [], "alg": [], "inst": set()})
+    for (name, kb), (kind, alg) in zip(disp, lau):
+        e = per[kind]
+        e["kb"].append(kb)
+        e["alg"].append(alg)
+        e["inst"].add(name)
+    return per
+
+
 def main():
-    fdir, wdir, out = sys.argv[1:4]
-    calib = float(sys.argv[4]) if len(sys.argv) > 4 else 8.0 * (1 << 24)
-    fetch = read(fdir, "FETCH_SIZE")
-    write = read(wdir, "WRITE_SIZE")
-    cf = [v for (k, _), vs in fetch.items() if k == "copy_axis" for v in vs]
-    cw = [v for (k, _), vs in write.items() if k == "copy_axis" for v in vs]
-    f_fac = calib / (1024.0 * (sum(cf) / len(cf))) if cf else 2.0
-    w_fac = calib / (1024.0 * (sum(cw) / len(cw))) if cw else 1.0
-    res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes)",
-           "calibration": {"kernel": "copy_axis", "known_bytes_each_way": calib,
+    workload, math, fdir, flog, wdir, wlog, out = sys.argv[1:8]
+    fetch = attribute(fdir, "FETCH_SIZE", flog)
+    write = attribute(wdir, "WRITE_SIZE", wlog)
+    cf, cw = fetch.pop("copy_axis", None), write.pop("copy_axis", None)
+    f_fac = CALIB_BYTES / (1024.0 * sum(cf["kb"]) / len(cf["kb"])) if cf else 2.0
+    w_fac = CALIB_BYTES / (1024.0 * sum(cw["kb"]) / len(cw["kb"])) if cw else 1.0
+    res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), "
+                     "dispatches attributed by the library's launch log",
+           "workload": workload, "math": math,
+           "calibration": {"kernel": "copy_axis", "known_bytes_each_way": CALIB_BYTES,
                            "fetch_factor": f_fac, "write_factor": w_fac,
                            "note": "bytes = counter_KB * 1024 * factor"},
            "kernels": {}}
-    for key in sorted(set(fetch) | set(write)):
-        k, mode = key
-        fv = fetch.get(key, [])
-        wv = write.get(key, [])
-        fb = (sum(fv) / len(fv)) * 1024.0 * f_fac if fv else None
-        wb = (sum(wv) / len(wv)) * 1024.0 * w_fac if wv else None
-        res["kernels"]["%s/%s" % (k, mode)] = {
+    for kind in sorted(set(fetch) | set(write)):
+        fv = fetch.get(kind, {"kb": []})["kb"]
+        wv = write.get(kind, {"kb": []})["kb"]
+        fb = sum(fv) / len(fv) * 1024.0 * f_fac if fv else None
+        wb = sum(wv) / len(wv) * 1024.0 * w_fac if wv else None
+        alg = fetch.get(kind) or write.get(kind)
+        algb = sum(alg["alg"]) / len(alg["alg"])
+        res["kernels"]["%s:%s/%s" % (workload, kind, math)] = {
             "launches": max(len(fv), len(wv)),
+            "instances": sorted((fetch.get(kind) or write.get(kind))["inst"]),
             "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
-            "hbm_bytes_per_launch": (fb or 0.0) + (wb or 0.0) if fb is not None and wb is not None else None,
-            "raw_fetch_kb_mean": (sum(fv) / len(fv)) if fv else None,
-            "raw_write_kb_mean": (sum(wv) / len(wv)) if wv else None}
+            "hbm_bytes_per_launch": fb + wb if fb is not None and wb is not None else None,
+            "algorithmic_bytes_per_launch": algb,
+            "traffic_over_algorithmic": (fb + wb) / algb if fb is not None and wb is not None
+            and algb else None}
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res, indent=1))

@@ -19,6 +19,8 @@ for f in sorted(glob.glob(os.path.join(d, "bench_*.json"))):
              rf["avg_launch_us"], rf["achieved"], 100 * rf["frac"], r["roundtrip_max_abs_err"]))
     for k, v in r.get("kernels", r.get("kernels_profiled_pass", {})).items():
         print("    %-16s n=%-4d avg %9.2f us  %7.1f GB/s" % (k, v["launches"], v["avg_us"], v["GBps"]))
+    if r.get("batched_wpt_strong"):
+        print("    wpt strong:", r["batched_wpt_strong"])
     if r.get("cpu_baseline"):
         print("    cpu:", r["cpu_baseline"])
 for f in sorted(glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True)):
