@@ -237,6 +237,31 @@ int jwv_wpt3d_fwd_f64(const double* x, double* y, int64_t p, int64_t q, int64_t 
 int jwv_wpt3d_rev_f64(const double* y, double* x, int64_t p, int64_t q, int64_t r, int lvl_p,
                       int lvl_q, int lvl_r, const jwv_taps* t, jwv_ctx* ctx);
 
+/* ---- AncientEgyptianDecomposition / decompose ----------------------------------
+ * transform: which BasicTransform is wrapped. */
+#define JWV_TRANSFORM_FWT 0 /* FastWaveletTransform */
+#define JWV_TRANSFORM_WPT 1 /* WaveletPacketTransform */
+/* AncientEgyptianDecomposition(transform).forward / reverse(double[])
+ * (transforms/AncientEgyptianDecomposition.java:97-184): any length n >= 1 is
+ * split into power-of-two pieces (MathToolKit.decompose, largest first,
+ * tools/MathToolKit.java:57-80), each transformed at full depth in place.
+ * Every piece <= 8192 samples runs in ONE varlen launch. */
+int jwv_aed_fwd_f64(const double* x, double* y, int64_t n, int transform, const jwv_taps* t,
+                    jwv_ctx* ctx);
+int jwv_aed_rev_f64(const double* y, double* x, int64_t n, int transform, const jwv_taps* t,
+                    jwv_ctx* ctx);
+int jwv_aed_fwd_f64_dev(const double* x, double* y, int64_t n, int transform,
+                        const jwv_taps* t, jwv_ctx* ctx);
+int jwv_aed_rev_f64_dev(const double* y, double* x, int64_t n, int transform,
+                        const jwv_taps* t, jwv_ctx* ctx);
+/* WaveletTransform.decompose(double[]) (transforms/WaveletTransform.java:136-145):
+ * mat receives (log2(n)+1) rows of n, row p = forward(x, p).  recompose(mat,
+ * level) (:173-182) is jwv_fwt_rev_f64 / jwv_wpt_rev_f64 on row `level`. */
+int jwv_decompose_f64(const double* x, double* mat, int64_t n, int transform,
+                      const jwv_taps* t, jwv_ctx* ctx);
+int jwv_decompose_f64_dev(const double* x, double* mat, int64_t n, int transform,
+                          const jwv_taps* t, jwv_ctx* ctx);
+
 /* ---- MODWT -------------------------------------------------------------------
  * MODWTTransform.forwardMODWT(double[] data, int maxLevel)  MODWTTransform.java:256-306
  *   wv receives (J+1)*n doubles, row-major [W_1 .. W_J, V_J] (coeffs[0..J]).

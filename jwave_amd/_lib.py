@@ -24,6 +24,8 @@ JWV_MATH_FMA = 1
 JWV_PLAN_CHAIN_REV = 1
 JWV_PLAN_CHAIN_FWD = 2
 JWV_PLAN_REV_HEAD = 4
+JWV_TRANSFORM_FWT = 0
+JWV_TRANSFORM_WPT = 1
 
 _dp = ctypes.c_void_p  # device or host double*
 _i64 = ctypes.c_int64
@@ -89,6 +91,10 @@ for _s in ("", "_dev"):
     _SIGS["jwv_compress_magnitude_f64%s" % _s] = [_dp, _dp, _i64, ctypes.c_double,
                                                   ctypes.POINTER(ctypes.c_double), _CTX]
     _SIGS["jwv_fwt_denoise_f64%s" % _s] = [_dp, _dp, _i64, _int, ctypes.c_double, _TP, _CTX]
+for _s in ("", "_dev"):
+    _SIGS["jwv_aed_fwd_f64%s" % _s] = [_dp, _dp, _i64, _int, _TP, _CTX]
+    _SIGS["jwv_aed_rev_f64%s" % _s] = [_dp, _dp, _i64, _int, _TP, _CTX]
+    _SIGS["jwv_decompose_f64%s" % _s] = [_dp, _dp, _i64, _int, _TP, _CTX]
 for _n in ("modwt_fwd", "modwt_inv"):
     for _s in ("", "_dev"):
         _SIGS["jwv_%s_f64%s" % (_n, _s)] = [_dp, _dp, _i64, _int, _TP, _CTX]

@@ -153,7 +153,7 @@ enum KernelKind {
   K_FWT_FWD_TILE, K_FWT_FWD_RES, K_FWT_REV_TILE, K_FWT_REV_RES, K_WPT_FWD_TILE, K_WPT_FWD_RES,
   K_WPT_REV_TILE, K_WPT_REV_RES, K_MODWT_FWD_TILE, K_MODWT_FWD_LEVEL, K_MODWT_INV_TILE,
   K_MODWT_INV_LEVEL, K_COPY, K_FWT_FWD_CHAIN, K_FWT_REV_CHAIN, K_FWT_REV_HEAD,
-  K_FWT_FWD_TILE_DEEP, K_FWT_REV_TILE_DEEP, K_NKINDS
+  K_FWT_FWD_TILE_DEEP, K_FWT_REV_TILE_DEEP, K_AED_VARLEN, K_NKINDS
 };
 // *_tile: the tiled pass that reads (forward) or writes (reverse) the full-length
 // axis — the HBM-bound launch; *_tile_deep: tiled passes over an intermediate
@@ -163,7 +163,7 @@ const char* const kKindNames[K_NKINDS] = {
     "fwt_fwd_tile", "fwt_fwd_res", "fwt_rev_tile", "fwt_rev_res", "wpt_fwd_tile", "wpt_fwd_res",
     "wpt_rev_tile", "wpt_rev_res", "modwt_fwd_tile", "modwt_fwd_level", "modwt_inv_tile",
     "modwt_inv_level", "copy_axis", "fwt_fwd_chain", "fwt_rev_chain", "fwt_rev_head",
-    "fwt_fwd_tile_deep", "fwt_rev_tile_deep"};
+    "fwt_fwd_tile_deep", "fwt_rev_tile_deep", "aed_varlen"};
 
 hipEvent_t take_event(jwv_ctx* c) {
   if (!c->ev_pool.empty()) {
@@ -717,6 +717,74 @@ void body_3d(jwv_ctx* c, Kind k, bool fwd, const Bank& b, const double* x, doubl
   }
 }
 
+// ------------------------------------------------ AncientEgyptianDecomposition
+// AncientEgyptianDecomposition.forward / reverse (AncientEgyptianDecomposition.
+// java:97-184): pieces of 2^p (MathToolKit.decompose, largest first,
+// MathToolKit.java:57-80), each through the wrapped transform's full-depth
+// forward / reverse (level p = calcExponent(2^p)).  Pieces up to the resident
+// cap go into ONE varlen launch (aed_kernels.hpp); larger ones take their own
+// pass plans.
+void check_aed(int64_t n) {
+  if (n < 1)  // MathToolKit.decompose (:61-64)
+    throw Fail{JWV_ERR_FAILURE, "the supported number for decomposition is smaller than one"};
+  if (n > 0x7fffffffLL) throw Fail{JWV_ERR_BAD_CALL, "array length exceeds the Java int range"};
+}
+
+void body_aed(jwv_ctx* c, Kind k, bool fwd, const Bank& b, const double* x, double* y,
+              int64_t n) {
+  jwv::VarSegs sg{};
+  int64_t off = 0;
+  for (int p = 62; p >= 0 && off < n; --p) {
+    const int64_t m = int64_t(1) << p;
+    if (((n - off) & m) == 0) continue;
+    if (m > Geo::kResCap1) {
+      body_1d(c, k, fwd, b, x + off, y + off, 1, m, m, p);
+    } else {
+      const int i = sg.count++;
+      sg.n[i] = (int)m;
+      sg.off[i] = off;
+      if (fwd) {
+        sg.h0[i] = (int)m;
+        sg.nlev[i] = fwd_levels((int)m, b.tw, p);
+      } else {
+        const int h = rev_first((int)m, b.tw, p);
+        sg.h0[i] = h ? h : (int)m;
+        sg.nlev[i] = h ? exponent(m / h) + 1 : 0;
+      }
+    }
+    off += m;
+  }
+  if (sg.count == 0) return;
+  jwv::VarArgs va{x, y, sg};
+  { ProfScope ps_(c, K_AED_VARLEN, 16.0 * (double)(n - (sg.count ? sg.off[0] : n)));
+    hipchk(jwv::launch_res_varlen(b, use_fma(c), k == Kind::WPT, fwd, va, c->stream),
+           "aed_varlen"); }
+}
+
+// WaveletTransform.decompose (WaveletTransform.java:136-145): row p =
+// forward(x, p), p = 0..log2 n.  Row p is row p-1 with ONE more level applied
+// (to the head [0, n >> (p-1)) for the FWT, to every packet of that size for
+// the WPT), so each row costs one level plus a copy of the untouched tail —
+// the same doubles as p separate forwards.
+void body_decompose(jwv_ctx* c, Kind k, const Bank& b, const double* x, double* mat, int64_t n) {
+  const int P = exponent(n);
+  hipchk(hipMemcpyAsync(mat, x, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, c->stream),
+         "decompose row 0");
+  for (int p = 1; p <= P; ++p) {
+    const int64_t h = n >> (p - 1);
+    const double* prev = mat + (int64_t)(p - 1) * n;
+    double* cur = mat + (int64_t)p * n;
+    if (k == Kind::FWT) {
+      body_1d(c, Kind::FWT, true, b, prev, cur, 1, h, h, 1);
+      if (h < n)
+        hipchk(hipMemcpyAsync(cur + h, prev + h, (size_t)(n - h) * sizeof(double),
+                              hipMemcpyDeviceToDevice, c->stream), "decompose tail");
+    } else {
+      body_1d(c, Kind::FWT, true, b, prev, cur, n / h, h, h, 1);  // Wavelet.forward per packet
+    }
+  }
+}
+
 // ------------------------------------------------------------------ MODWT
 // MODWTTransform.initializeFilterCache / normalize (MODWTTransform.java:452-484,
 // 599-606); evaluated in the same order, compiled with -ffp-contract=off.
@@ -966,6 +1034,10 @@ hipError_t launch_wpt_rev_tile(const Bank& b, bool fma, int C, const TileArgs& a
     return e;
   if (a.K > Geo::wpt_k(C) || a.h < Geo::wpt_t(C)) return hipErrorInvalidValue;
   JWV_MODE2(wpt_rev_tile, b, C, a, s);
+}
+hipError_t launch_res_varlen(const Bank& b, bool fma, bool wpt, bool fwd, const VarArgs& a,
+                             hipStream_t s) {
+  JWV_MODE2(res_varlen, b, wpt, fwd, a, s);
 }
 hipError_t launch_modwt_fwd(const Bank& b, bool fma, bool tiled, const ModwtArgs& a,
                             hipStream_t s) {
@@ -1373,6 +1445,65 @@ int jwv_fwt_denoise_f64_dev(const double* x, double* y, int64_t n, int level, do
     body_denoise(c, b, x, y, n, level, threshold);
   });
 }
+
+// ---- AncientEgyptianDecomposition / decompose ------------------------------------
+static Kind kind_of_transform(int transform) {
+  if (transform == JWV_TRANSFORM_FWT) return Kind::FWT;
+  if (transform == JWV_TRANSFORM_WPT) return Kind::WPT;
+  throw Fail{JWV_ERR_BAD_CALL, "unknown transform (JWV_TRANSFORM_FWT | JWV_TRANSFORM_WPT)"};
+}
+#define JWV_AED(NAME, FWD, DEV)                                                                 \
+  int NAME(const double* x, double* y, int64_t n, int transform, const jwv_taps* t,           \
+           jwv_ctx* c) {                                                                       \
+    return guarded(c, [&] {                                                                    \
+      const Bank b = make_bank(t);                                                             \
+      const Kind k = kind_of_transform(transform);                                             \
+      check_aed(n);                                                                            \
+      if (DEV) {                                                                               \
+        need_device_ptrs(c, x, y);                                                             \
+        check_overlap(x, (size_t)n, y, (size_t)n);                                             \
+        body_aed(c, k, FWD, b, x, y, n);                                                       \
+      } else {                                                                                 \
+        check_ptrs(x, y);                                                                      \
+        staged(c, x, (size_t)n, y, (size_t)n,                                                  \
+               [&](const double* dx, double* dy) { body_aed(c, k, FWD, b, dx, dy, n); });      \
+      }                                                                                        \
+    });                                                                                        \
+  }
+JWV_AED(jwv_aed_fwd_f64, true, false)
+JWV_AED(jwv_aed_rev_f64, false, false)
+JWV_AED(jwv_aed_fwd_f64_dev, true, true)
+JWV_AED(jwv_aed_rev_f64_dev, false, true)
+
+// BasicTransform#calcExponent's check (BasicTransform.java:688-697)
+static void check_decompose(int64_t n) {
+  if (!is_binary(n))
+    throw Fail{JWV_ERR_FAILURE, "BasicTransform#calcExponent - given number is not binary: "
+                                "2^p | pEN .. = 1, 2, 4, 8, 16, 32, .. "};
+  if (n > (int64_t(1) << 30))
+    throw Fail{JWV_ERR_BAD_CALL, "signal length exceeds the Java int array range (2^30)"};
+}
+#define JWV_DECOMP(NAME, DEV)                                                                   \
+  int NAME(const double* x, double* mat, int64_t n, int transform, const jwv_taps* t,         \
+           jwv_ctx* c) {                                                                       \
+    return guarded(c, [&] {                                                                    \
+      const Bank b = make_bank(t);                                                             \
+      const Kind k = kind_of_transform(transform);                                             \
+      check_decompose(n);                                                                      \
+      const size_t rows = (size_t)exponent(n) + 1;                                             \
+      if (DEV) {                                                                               \
+        need_device_ptrs(c, x, mat);                                                           \
+        check_overlap(x, (size_t)n, mat, rows * (size_t)n);                                    \
+        body_decompose(c, k, b, x, mat, n);                                                    \
+      } else {                                                                                 \
+        check_ptrs(x, mat);                                                                    \
+        staged(c, x, (size_t)n, mat, rows * (size_t)n,                                         \
+               [&](const double* dx, double* dy) { body_decompose(c, k, b, dx, dy, n); });     \
+      }                                                                                        \
+    });                                                                                        \
+  }
+JWV_DECOMP(jwv_decompose_f64, false)
+JWV_DECOMP(jwv_decompose_f64_dev, true)
 
 // ---- MODWT -------------------------------------------------------------------------
 int jwv_modwt_filters(const jwv_taps* t, double* g, double* h) {

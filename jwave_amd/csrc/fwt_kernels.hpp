@@ -234,18 +234,12 @@ __device__ double rev_small(const typename FB<L>::Rev& tp, const double* a, cons
 // barriers: a deep tail is latency-bound).
 // ====================================================================
 template <int L, int C, int NT, int CAP, bool FMA>
-__global__ __launch_bounds__(NT) void fwt_fwd_res(const double* __restrict__ src, AxisView sv,
-                                                  double* __restrict__ dst, AxisView dv, int h0,
-                                                  int nlev, int inner, int dma,
-                                                  typename FB<L>::Fwd tp) {
+__device__ __forceinline__ void fwt_fwd_res_blk(const double* __restrict__ s, AxisView sv,
+    double* __restrict__ y, AxisView dv, int h0, int nlev, int c0, int inner, int dma,
+    const typename FB<L>::Fwd& tp) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   constexpr int MAXP = (CAP / 2 * C + NT - 1) / NT;
   constexpr int MAXU = (CAP * C + NT - 1) / NT;
-  const int ncb = (inner + C - 1) / C;
-  const int64_t o = blockIdx.x / ncb;
-  const int c0 = (blockIdx.x % ncb) * C;
-  const double* s = src + view_base(sv, o) + c0;
-  double* y = dst + view_base(dv, o) + c0;
   const int tid = threadIdx.x;
   JWV_STAMP(0);
   load_window<C, NT, MAXU>(lds, s, h0, dma != 0, c0, inner,
@@ -297,6 +291,18 @@ __global__ __launch_bounds__(NT) void fwt_fwd_res(const double* __restrict__ src
     if (c0 + c < inner) y[(int64_t)i * dv.s_len + c] = lds[q];
   }
   JWV_STAMP(42);
+}
+
+template <int L, int C, int NT, int CAP, bool FMA>
+__global__ __launch_bounds__(NT) void fwt_fwd_res(const double* __restrict__ src, AxisView sv,
+    double* __restrict__ dst, AxisView dv, int h0, int nlev, int inner, int dma,
+    typename FB<L>::Fwd tp) {
+  const int ncb = (inner + C - 1) / C;
+  const int64_t o = blockIdx.x / ncb;
+  const int c0 = (blockIdx.x % ncb) * C;
+  const double* s = src + view_base(sv, o) + c0;
+  double* y = dst + view_base(dv, o) + c0;
+  fwt_fwd_res_blk<L, C, NT, CAP, FMA>(s, sv, y, dv, h0, nlev, c0, inner, dma, tp);
 }
 
 // ====================================================================
@@ -498,20 +504,14 @@ __device__ __forceinline__ void rev_pair_any(const typename FB<L>::Rev& tp, int 
 // most 64 pairs (the first ones) run on wave 0 alone.
 // ====================================================================
 template <int L, int C, int NT, int CAP, bool FMA>
-__global__ __launch_bounds__(NT) void fwt_rev_res(const double* __restrict__ src, AxisView sv,
-                                                  double* __restrict__ dst, AxisView dv, int h0,
-                                                  int nlev, int inner, int dma,
-                                                  typename FB<L>::Rev tp) {
+__device__ __forceinline__ void fwt_rev_res_blk(const double* __restrict__ s, AxisView sv,
+    double* __restrict__ y, AxisView dv, int h0, int nlev, int c0, int inner, int dma,
+    const typename FB<L>::Rev& tp) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   constexpr int MAXP = (CAP / 2 * C + NT - 1) / NT;
   constexpr int MAXU = (CAP * C + NT - 1) / NT;
   const int nL = FB<L>::nr(tp);
   const int qe = (nL + 1) >> 1;
-  const int ncb = (inner + C - 1) / C;
-  const int64_t o = blockIdx.x / ncb;
-  const int c0 = (blockIdx.x % ncb) * C;
-  const double* s = src + view_base(sv, o) + c0;
-  double* y = dst + view_base(dv, o) + c0;
   const int tid = threadIdx.x;
   const int htop = nlev > 0 ? (h0 << (nlev - 1)) : h0;
 
@@ -612,6 +612,18 @@ __global__ __launch_bounds__(NT) void fwt_rev_res(const double* __restrict__ src
     if (c0 + c < inner) y[(int64_t)i * dv.s_len + c] = lds[q];
   }
   JWV_STAMP(42);
+}
+
+template <int L, int C, int NT, int CAP, bool FMA>
+__global__ __launch_bounds__(NT) void fwt_rev_res(const double* __restrict__ src, AxisView sv,
+    double* __restrict__ dst, AxisView dv, int h0, int nlev, int inner, int dma,
+    typename FB<L>::Rev tp) {
+  const int ncb = (inner + C - 1) / C;
+  const int64_t o = blockIdx.x / ncb;
+  const int c0 = (blockIdx.x % ncb) * C;
+  const double* s = src + view_base(sv, o) + c0;
+  double* y = dst + view_base(dv, o) + c0;
+  fwt_rev_res_blk<L, C, NT, CAP, FMA>(s, sv, y, dv, h0, nlev, c0, inner, dma, tp);
 }
 
 // ====================================================================

@@ -48,6 +48,17 @@ struct AxisView {
   int32_t pad_;
 };
 
+// Segments of one AncientEgyptianDecomposition varlen launch (aed_kernels.hpp),
+// passed by value in the kernel arguments.
+struct VarSegs {
+  static constexpr int kMax = 32;
+  int count;
+  int n[kMax];     // segment length (a power of two)
+  int h0[kMax];    // FWT fwd: level input size; FWT/WPT rev: first synthesis size
+  int nlev[kMax];  // levels (0 = copy)
+  int64_t off[kMax];
+};
+
 __device__ __forceinline__ int64_t view_base(const AxisView& v, int64_t o) {
   if (v.pk == 1) return o * v.s_outer;
   return (o / v.pk) * v.s_outer + (o % v.pk) * v.s_pk;

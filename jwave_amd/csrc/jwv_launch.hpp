@@ -51,6 +51,13 @@ struct TileArgs {  // tiled FWT/WPT kernels
   int sp = 0;  // cache policy of the full-length output stores (st2_pol), C = 1 kernels
   int t1 = 0;  // C = 1 forward tile: 0 = Geo::kFwt1T, or 1024 (first pass of a long signal)
 };
+// AncientEgyptianDecomposition varlen launch (aed_kernels.hpp): contiguous
+// 1-D segments of src / dst, one block each.
+struct VarArgs {
+  const double* src;
+  double* dst;
+  const VarSegs& seg;
+};
 struct ModwtArgs {
   const double* src;  // fwd: V_{j0-1}; inv: V_{j1}
   const double* coef; // inv: W rows base
@@ -155,6 +162,8 @@ hipError_t launch_modwt_fwd(const Bank& modwt_gh, bool fma, bool tiled, const Mo
                             hipStream_t);
 hipError_t launch_modwt_inv(const Bank& modwt_gh, bool fma, bool tiled, const ModwtArgs&,
                             hipStream_t);
+hipError_t launch_res_varlen(const Bank&, bool fma, bool wpt, bool fwd, const VarArgs&,
+                             hipStream_t);
 hipError_t launch_copy_axis(const double* src, AxisView sv, double* dst, AxisView dv,
                             int64_t nouter, int len, int inner, hipStream_t);
 
@@ -188,6 +197,7 @@ hipError_t wpt_fwd_tile(const Bank&, int C, const TileArgs&, hipStream_t);
 hipError_t wpt_rev_tile(const Bank&, int C, const TileArgs&, hipStream_t);
 hipError_t modwt_fwd(const Bank&, bool tiled, const ModwtArgs&, hipStream_t);
 hipError_t modwt_inv(const Bank&, bool tiled, const ModwtArgs&, hipStream_t);
+hipError_t res_varlen(const Bank&, bool wpt, bool fwd, const VarArgs&, hipStream_t);
 }  // namespace exact
 namespace fused {
 hipError_t fwt_rev_head(const Bank&, const RevHeadArgs&, hipStream_t);
@@ -210,6 +220,7 @@ hipError_t wpt_fwd_tile(const Bank&, int C, const TileArgs&, hipStream_t);
 hipError_t wpt_rev_tile(const Bank&, int C, const TileArgs&, hipStream_t);
 hipError_t modwt_fwd(const Bank&, bool tiled, const ModwtArgs&, hipStream_t);
 hipError_t modwt_inv(const Bank&, bool tiled, const ModwtArgs&, hipStream_t);
+hipError_t res_varlen(const Bank&, bool wpt, bool fwd, const VarArgs&, hipStream_t);
 }  // namespace fused
 
 }  // namespace jwv

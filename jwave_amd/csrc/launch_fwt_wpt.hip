@@ -2,7 +2,8 @@
 // Compiled twice: -DJWV_FMA=0 (namespace jwv::exact) and -DJWV_FMA=1
 // (namespace jwv::fused).  Grid/LDS geometry comes from jwv::Geo.
 #include "jwv_launch.hpp"
-#include "wpt_kernels.hpp"
+#include "aed_kernels.hpp"
+#include <type_traits>
 
 #ifndef JWV_FMA
 #error "JWV_FMA must be 0 or 1"
@@ -237,6 +238,33 @@ hipError_t wpt_rev_tile_go(const Bank& b, const TileArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------- AED varlen
+template <int L, int OP>
+hipError_t res_var_go(const Bank& b, const VarArgs& a, hipStream_t s) {
+  constexpr bool fwd = OP == 0 || OP == 2;
+  using TP = typename std::conditional<fwd, typename FB<L>::Fwd, typename FB<L>::Rev>::type;
+  auto k = res_varlen<L, NT, cap<1>(), kFMA, OP, TP>;
+  int mx = 0;
+  for (int i = 0; i < a.seg.count; ++i) mx = a.seg.n[i] > mx ? a.seg.n[i] : mx;
+  const size_t lds = (size_t)(mx + 2) * sizeof(double);
+  if (hipError_t e = prep(k, lds)) return e;
+  TP tp;
+  if constexpr (fwd) tp = fwd_taps<L>(b); else tp = rev_taps<L>(b);
+  hipLaunchKernelGGL(k, dim3((unsigned)a.seg.count), dim3(NT), lds, s, a.src, a.dst, a.seg, tp);
+  return hipGetLastError();
+}
+template <int OP>
+hipError_t res_var_l(const Bank& b, const VarArgs& a, hipStream_t s) {
+  const bool rev = OP == 1 || OP == 3;
+  switch ((rev && b.scale != 1.0) ? 0 : static_l(b.L)) {
+    case 2: return res_var_go<2, OP>(b, a, s);
+    case 4: return res_var_go<4, OP>(b, a, s);
+    case 8: return res_var_go<8, OP>(b, a, s);
+    case 16: return res_var_go<16, OP>(b, a, s);
+    default: return res_var_go<0, OP>(b, a, s);
+  }
+}
+
 }  // namespace
 
 // L dispatch: compiled-in tap counts, else the runtime-L kernels.  A scaled
@@ -286,6 +314,11 @@ hipError_t wpt_fwd_tile(const Bank& b, int C, const TileArgs& a, hipStream_t s) 
 }
 hipError_t wpt_rev_tile(const Bank& b, int C, const TileArgs& a, hipStream_t s) {
   JWV_DISPATCH(wpt_rev_tile_go, b, C, a, s, true);
+}
+hipError_t res_varlen(const Bank& b, bool wpt, bool fwd, const VarArgs& a, hipStream_t s) {
+  if (a.seg.count < 1 || a.seg.count > VarSegs::kMax) return hipErrorInvalidValue;
+  if (!wpt) return fwd ? res_var_l<0>(b, a, s) : res_var_l<1>(b, a, s);
+  return fwd ? res_var_l<2>(b, a, s) : res_var_l<3>(b, a, s);
 }
 }  // namespace JWV_NS
 

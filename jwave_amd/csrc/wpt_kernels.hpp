@@ -20,18 +20,12 @@ namespace jwv {
 
 // ---------------------------------------------------------------- forward
 template <int L, int C, int NT, int CAP, bool FMA>
-__global__ __launch_bounds__(NT) void wpt_fwd_res(const double* __restrict__ src, AxisView sv,
-                                                  double* __restrict__ dst, AxisView dv, int n,
-                                                  int nlev, int inner, int dma,
-                                                  typename FB<L>::Fwd tp) {
+__device__ __forceinline__ void wpt_fwd_res_blk(const double* __restrict__ s, AxisView sv,
+    double* __restrict__ y, AxisView dv, int n, int nlev, int c0, int inner, int dma,
+    const typename FB<L>::Fwd& tp) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   constexpr int MAXP = (CAP / 2 * C + NT - 1) / NT;
   constexpr int MAXU = (CAP * C + NT - 1) / NT;
-  const int ncb = (inner + C - 1) / C;
-  const int64_t o = blockIdx.x / ncb;
-  const int c0 = (blockIdx.x % ncb) * C;
-  const double* s = src + view_base(sv, o) + c0;
-  double* y = dst + view_base(dv, o) + c0;
   const int tid = threadIdx.x;
   load_window<C, NT, MAXU>(lds, s, n, dma != 0, c0, inner,
                            [&](int e) { return (int64_t)e * sv.s_len; });
@@ -70,6 +64,18 @@ __global__ __launch_bounds__(NT) void wpt_fwd_res(const double* __restrict__ src
     const int i = q / C, c = q % C;
     if (c0 + c < inner) y[(int64_t)i * dv.s_len + c] = lds[q];
   }
+}
+
+template <int L, int C, int NT, int CAP, bool FMA>
+__global__ __launch_bounds__(NT) void wpt_fwd_res(const double* __restrict__ src, AxisView sv,
+    double* __restrict__ dst, AxisView dv, int n, int nlev, int inner, int dma,
+    typename FB<L>::Fwd tp) {
+  const int ncb = (inner + C - 1) / C;
+  const int64_t o = blockIdx.x / ncb;
+  const int c0 = (blockIdx.x % ncb) * C;
+  const double* s = src + view_base(sv, o) + c0;
+  double* y = dst + view_base(dv, o) + c0;
+  wpt_fwd_res_blk<L, C, NT, CAP, FMA>(s, sv, y, dv, n, nlev, c0, inner, dma, tp);
 }
 
 // Tiled: signal (or packet) length h, tile t covers [tT, tT+T).  After level
@@ -148,19 +154,13 @@ __global__ __launch_bounds__(NT) void wpt_fwd_tile(const double* __restrict__ sr
 // Resident: signal/packet of length n; reverse levels with packet sizes
 // h0, 2h0, .., h0 << (nlev-1) (<= n).  Every packet of size h is reversed in place.
 template <int L, int C, int NT, int CAP, bool FMA>
-__global__ __launch_bounds__(NT) void wpt_rev_res(const double* __restrict__ src, AxisView sv,
-                                                  double* __restrict__ dst, AxisView dv, int n,
-                                                  int h0, int nlev, int inner, int dma,
-                                                  typename FB<L>::Rev tp) {
+__device__ __forceinline__ void wpt_rev_res_blk(const double* __restrict__ s, AxisView sv,
+    double* __restrict__ y, AxisView dv, int n, int h0, int nlev, int c0, int inner,
+    int dma, const typename FB<L>::Rev& tp) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   constexpr int MAXP = (CAP / 2 * C + NT - 1) / NT;
   constexpr int MAXU = (CAP * C + NT - 1) / NT;
   const int nL = FB<L>::nr(tp);
-  const int ncb = (inner + C - 1) / C;
-  const int64_t o = blockIdx.x / ncb;
-  const int c0 = (blockIdx.x % ncb) * C;
-  const double* s = src + view_base(sv, o) + c0;
-  double* y = dst + view_base(dv, o) + c0;
   const int tid = threadIdx.x;
   load_window<C, NT, MAXU>(lds, s, n, dma != 0, c0, inner,
                            [&](int e) { return (int64_t)e * sv.s_len; });
@@ -210,6 +210,18 @@ __global__ __launch_bounds__(NT) void wpt_rev_res(const double* __restrict__ src
     const int i = q / C, c = q % C;
     if (c0 + c < inner) y[(int64_t)i * dv.s_len + c] = lds[q];
   }
+}
+
+template <int L, int C, int NT, int CAP, bool FMA>
+__global__ __launch_bounds__(NT) void wpt_rev_res(const double* __restrict__ src, AxisView sv,
+    double* __restrict__ dst, AxisView dv, int n, int h0, int nlev, int inner, int dma,
+    typename FB<L>::Rev tp) {
+  const int ncb = (inner + C - 1) / C;
+  const int64_t o = blockIdx.x / ncb;
+  const int c0 = (blockIdx.x % ncb) * C;
+  const double* s = src + view_base(sv, o) + c0;
+  double* y = dst + view_base(dv, o) + c0;
+  wpt_rev_res_blk<L, C, NT, CAP, FMA>(s, sv, y, dv, n, h0, nlev, c0, inner, dma, tp);
 }
 
 // Tiled reverse: K levels, packet sizes hK>>(K-1) .. hK (hK = signal/packet

@@ -280,6 +280,8 @@ def transform_axis(x, wavelet, level, axis_len_dim=1, forward=True, ctx=None, ki
 
 
 def modwt_forward(x, wavelet, J, ctx=None):
+    if not _is_torch(x):
+        x = np.ascontiguousarray(np.asarray(x, dtype=np.float64))
     n = x.shape[0]
     return _run("jwv_modwt_fwd_f64", "jwv_modwt_fwd_f64_dev", ctx, x, (int(J) + 1, n),
                 (n, int(J), _TapsHolder.of(wavelet)))
@@ -290,6 +292,32 @@ def modwt_inverse(coeffs, wavelet, ctx=None):
     n = coeffs.shape[1]
     return _run("jwv_modwt_inv_f64", "jwv_modwt_inv_f64_dev", ctx, coeffs, (n,),
                 (n, int(J), _TapsHolder.of(wavelet)))
+
+
+def _transform_id(kind):
+    return {"fwt": L.JWV_TRANSFORM_FWT, "wpt": L.JWV_TRANSFORM_WPT}[kind]
+
+
+def aed_transform(x, wavelet, kind, forward, ctx=None):
+    """AncientEgyptianDecomposition(FWT | WPT).forward / reverse of an array
+    of any length >= 1 (jwv_aed_*: AncientEgyptianDecomposition.java:97-184)."""
+    if not _is_torch(x):
+        x = np.ascontiguousarray(np.asarray(x, dtype=np.float64))
+    n = int(x.shape[0])
+    d = "fwd" if forward else "rev"
+    return _run("jwv_aed_%s_f64" % d, "jwv_aed_%s_f64_dev" % d, ctx, x, (n,),
+                (n, _transform_id(kind), _TapsHolder.of(wavelet)))
+
+
+def decompose(x, wavelet, kind="fwt", ctx=None):
+    """WaveletTransform.decompose (WaveletTransform.java:136-145): a
+    (log2 n + 1) x n matrix, row p = forward(x, p); one native call."""
+    if not _is_torch(x):
+        x = np.ascontiguousarray(np.asarray(x, dtype=np.float64))
+    n = int(x.shape[0])
+    rows = (n.bit_length() if n > 0 else 1)  # log2 n + 1 for powers of two
+    return _run("jwv_decompose_f64", "jwv_decompose_f64_dev", ctx, x, (rows, n),
+                (n, _transform_id(kind), _TapsHolder.of(wavelet)))
 
 
 def compress_magnitude(x, threshold=1.0, ctx=None):
@@ -484,9 +512,9 @@ class WaveletTransform(BasicTransform):
 
     # WaveletTransform.decompose / recompose (:136-182)
     def decompose(self, arr):
-        n = arr.shape[0]
-        levels = get_exponent(n)
-        return np.stack([np.asarray(self.forward_1d(arr, p)) for p in range(levels + 1)])
+        """All levels at once: row p = forward(arr, p), p = 0..log2 n, one
+        native call (jwv_decompose_f64)."""
+        return decompose(arr, self._wavelet, self.kind, self._ctx)
 
     def recompose(self, mat, level=None):
         if level is None:
@@ -564,6 +592,13 @@ def _check_modwt_levels(n, J):
                              " %d" % (J, theo, n))
 
 
+def _zeros_like_input(a, n):
+    if _is_torch(a):
+        import torch
+        return torch.zeros(n, dtype=torch.float64, device=a.device)
+    return np.zeros(n)
+
+
 class MODWTTransform(WaveletTransform):
     """MODWTTransform.java:104-913 (DIRECT convolution semantics)."""
 
@@ -592,34 +627,61 @@ class MODWTTransform(WaveletTransform):
         c = np.ascontiguousarray(np.asarray(coefficients, dtype=np.float64))
         return modwt_inverse(c, self._wavelet, self._ctx)
 
-    # flattened pow-2 API (:389-443)
+    # flattened pow-2 API: forward/reverse(double[], int) :389-443 and the
+    # single-argument forward/reverse(double[]) :854-912
     def forward_1d(self, arr, level=None):
         n = len(arr)
         if n == 0:
-            return np.zeros(0)
-        if not is_binary(n):
-            raise JWaveFailure("MODWTTransform#forward - given array length is not 2^p | p E N"
-                               " ... = 1, 2, 4, 8, 16, 32, .. ")
-        if level is None:
+            return _zeros_like_input(arr, 0)
+        if level is None:  # :854-870: calcExponent, then forwardMODWT at full depth
+            if not is_binary(n):
+                raise JWaveFailure("BasicTransform#calcExponent - given number is not binary: "
+                                   "2^p | pEN .. = 1, 2, 4, 8, 16, 32, .. ")
             level = get_exponent(n)
-        if level < 0 or level > get_exponent(n):
-            raise JWaveFailure("MODWTTransform#forward - given level is out of range for given"
-                               " array")
-        if level > MAX_DECOMPOSITION_LEVEL:
-            raise JWaveFailure("MODWTTransform#forward - maximum supported decomposition level is"
-                               " %d, requested: %d" % (MAX_DECOMPOSITION_LEVEL, level))
-        return np.asarray(self.forwardMODWT(arr, level)).reshape(-1)
+        else:  # :389-404
+            if not is_binary(n):
+                raise JWaveFailure("MODWTTransform#forward - given array length is not 2^p | p E N"
+                                   " ... = 1, 2, 4, 8, 16, 32, .. ")
+            if level < 0 or level > get_exponent(n):
+                raise JWaveFailure("MODWTTransform#forward - given level is out of range for given"
+                                   " array")
+            if level > MAX_DECOMPOSITION_LEVEL:
+                raise JWaveFailure("MODWTTransform#forward - maximum supported decomposition level"
+                                   " is %d, requested: %d" % (MAX_DECOMPOSITION_LEVEL, level))
+        # [W_1 .. W_J, V_J] rows of N, flattened (:406-416)
+        return self.forwardMODWT(arr, level).reshape(-1)
 
     def reverse_1d(self, arr, level=None):
-        if len(arr) == 0:
-            return np.zeros(0)
-        n = len(arr) // (level + 1)
-        if not is_binary(n):
-            raise JWaveFailure("MODWTTransform#reverse - Invalid coefficient array for given level")
-        if len(arr) != n * (level + 1):
-            raise JWaveFailure("MODWTTransform#reverse - Coefficient array length does not match"
-                               " expected size for given level")
-        return self.inverseMODWT(np.asarray(arr).reshape(level + 1, n))
+        total = len(arr)
+        if total == 0:
+            return _zeros_like_input(arr, 0)
+        if level is None:
+            # :880-902: the first N (ascending) with N | total, N = 2^p and
+            # total/N - 1 <= p; ambiguous by design (N=16,J=1 reads as N=8,J=3,
+            # SURVEY Appendix A.6) — reproduced, not "fixed".  Only powers of
+            # two can pass isBinary, so they are the only candidates tried.
+            n = levels = 0
+            p = 0
+            while (1 << p) <= total:
+                t = 1 << p
+                if total % t == 0 and 0 <= total // t - 1 <= p:
+                    n, levels = t, total // t - 1
+                    break
+                p += 1
+            if n == 0:
+                raise JWaveFailure("MODWTTransform#reverse - Invalid flattened coefficient array "
+                                   "length. Cannot determine original signal dimensions.")
+            level = levels
+        else:  # :419-443
+            n = total // (level + 1)
+            if not is_binary(n):
+                raise JWaveFailure("MODWTTransform#reverse - Invalid coefficient array for given "
+                                   "level")
+            if total != n * (level + 1):
+                raise JWaveFailure("MODWTTransform#reverse - Coefficient array length does not "
+                                   "match expected size for given level")
+        return self.inverseMODWT(arr.reshape(level + 1, n) if _is_torch(arr)
+                                 else np.asarray(arr, dtype=np.float64).reshape(level + 1, n))
 
     def _check_1d(self, n, level, fwd):
         pass
@@ -669,6 +731,10 @@ class AncientEgyptianDecomposition(BasicTransform):
 
     def _run(self, a, fwd):
         n = a.shape[0]
+        if getattr(self._basic, "kind", None) in ("fwt", "wpt"):
+            # one native call: every piece <= 8192 in one varlen launch
+            return aed_transform(a, self._basic.getWavelet(), self._basic.kind, fwd,
+                                 self._basic._ctx)
         if _is_torch(a):
             import torch
             out = torch.empty_like(a)

@@ -483,34 +483,203 @@ def test_axis_columns(ctx, kind, wname, R, cw, lev):
     assert_exact(y3[0].cpu().numpy(), ref, "%s axis fwd 3d" % kind)
 
 
+@pytest.mark.parametrize("kind", ["fwt", "wpt"])
 @pytest.mark.parametrize("wname,n", [("Daubechies4", 1000), ("Haar1", 127), ("Symlet8", 70000),
-                                     ("Daubechies8", 1), ("Daubechies2", 3)])
-def test_ancient_egyptian_decomposition(ctx, wname, n):
-    """AncientEgyptianDecomposition over the native FWT
-    (AncientEgyptianDecomposition.java:97-184): every power-of-two sub-array
-    through the full-depth forward/reverse, bit-exact vs the oracle applied
-    to the same sub-arrays; numpy and device tensors."""
+                                     ("Daubechies8", 1), ("Daubechies2", 3),
+                                     ("Coiflet1", 8191), ("Haar1Orthogonal", 24577),
+                                     ("Daubechies20", 12345), ("Daubechies4", (1 << 20) + 8191)])
+def test_ancient_egyptian_decomposition(ctx, kind, wname, n):
+    """AncientEgyptianDecomposition over the native FWT / WPT
+    (AncientEgyptianDecomposition.java:97-184) through jwv_aed_*: every
+    power-of-two sub-array through the full-depth forward/reverse — the pieces
+    up to 8192 in ONE varlen launch, larger ones on their own plans — bit-exact
+    vs the oracle applied to the same sub-arrays; numpy and device tensors."""
     import torch
     w = jw.by_class(wname)
-    aed = jw.AncientEgyptianDecomposition(jw.FastWaveletTransform(w, ctx))
+    basic = jw.FastWaveletTransform(w, ctx) if kind == "fwt" else jw.WaveletPacketTransform(w, ctx)
+    aed = jw.AncientEgyptianDecomposition(basic)
+    fwd = oracle.fwt_forward if kind == "fwt" else oracle.wpt_forward
+    rev = oracle.fwt_reverse if kind == "fwt" else oracle.wpt_reverse
     x = rnd(n, seed=11)
     ref = np.empty(n)
     off = 0
     for p in jw.decompose_number(n):
         m = 1 << p
-        ref[off:off + m] = oracle.fwt_forward(w, x[off:off + m], p)
+        ref[off:off + m] = fwd(w, x[off:off + m], p)
         off += m
     y = aed.forward(x)
-    assert_exact(y, ref, "aed fwd")
+    assert_exact(y, ref, "aed %s fwd" % kind)
     back = np.empty(n)
     off = 0
     for p in jw.decompose_number(n):
         m = 1 << p
-        back[off:off + m] = oracle.fwt_reverse(w, ref[off:off + m], p)
+        back[off:off + m] = rev(w, ref[off:off + m], p)
         off += m
-    assert_exact(aed.reverse(ref), back, "aed rev")
+    assert_exact(aed.reverse(ref), back, "aed %s rev" % kind)
     yd = aed.forward(torch.from_numpy(x).cuda())
-    assert_exact(yd.cpu().numpy(), ref, "aed fwd device")
+    assert_exact(yd.cpu().numpy(), ref, "aed %s fwd device" % kind)
+
+
+def test_aed_one_varlen_launch(ctx):
+    """n = 2^20 + 8191: the 2^20 piece on its pass plan, the 13 pieces of
+    8191 = 4096 + .. + 1 in ONE launch (not 13)."""
+    w = jw.by_class("Daubechies4")
+    x = rnd((1 << 20) + 8191, seed=3)
+    ctx.profile(True)
+    try:
+        T.aed_transform(x, w, "fwt", True, ctx)
+        prof = ctx.profile_read()
+    finally:
+        ctx.profile(False)
+    assert prof["aed_varlen"]["launches"] == 1
+    with pytest.raises(jw.JWaveFailure, match="smaller than one"):
+        T.aed_transform(np.zeros(0), w, "fwt", True, ctx)
+
+
+# ------------------------------------------------------- decompose / recompose
+@pytest.mark.parametrize("kind", ["fwt", "wpt"])
+@pytest.mark.parametrize("wname", ["Haar1", "Daubechies4", "Symlet8", "Coiflet1", "Daubechies20",
+                                   "Haar1Orthogonal", "BiOrthogonal35", "CDF53"])
+def test_decompose_recompose(ctx, kind, wname):
+    """WaveletTransform.decompose / recompose (WaveletTransform.java:136-182)
+    in one native call (jwv_decompose_f64): row p == forward(x, p) of the
+    oracle, bit-exact, for every level; recompose(mat, level) from every
+    level == the oracle's reverse(row, level)."""
+    w = jw.by_class(wname)
+    fwd = oracle.fwt_forward if kind == "fwt" else oracle.wpt_forward
+    rev = oracle.fwt_reverse if kind == "fwt" else oracle.wpt_reverse
+    t = jw.FastWaveletTransform(w, ctx) if kind == "fwt" else jw.WaveletPacketTransform(w, ctx)
+    for n in (1, 2, 4, 64, 1024, 1 << 15):
+        x = rnd(n, seed=n + 5)
+        mat = t.decompose(x)
+        assert mat.shape == (n.bit_length(), n)
+        for p in range(n.bit_length()):
+            ref = fwd(w, x, p)
+            assert_exact(mat[p], ref, "%s %s decompose n=%d row %d" % (kind, wname, n, p))
+            assert_exact(t.recompose(mat, p), rev(w, ref, p),
+                         "%s %s recompose n=%d level %d" % (kind, wname, n, p))
+        assert_exact(t.recompose(mat), rev(w, mat[-1], n.bit_length() - 1), "recompose()")
+
+
+def test_decompose_kat_gpu(ctx):
+    """DecomposeTest.testDecompose (DecomposeTest.java:30-170) on the GPU for
+    every create2arr wavelet: constant signals of 4 and 64, the expected
+    orthonormal pyramids (delta 1e-8), recompose from every level."""
+    s2 = np.sqrt(2.0)
+    exp4 = np.array([[1, 1, 1, 1], [s2, s2, 0, 0], [2, 0, 0, 0]], dtype=float)
+    exp64 = np.zeros((7, 64))
+    for p in range(7):
+        m = 64 >> p
+        exp64[p, :m] = 2.0 ** (p / 2.0)
+    exp64[0] = 1.0
+    for w in jw.WaveletBuilder.create2arr():
+        t = jw.Transform(jw.FastWaveletTransform(w, ctx))
+        for x, exp in ((np.ones(4), exp4), (np.ones(64), exp64)):
+            mat = t.decompose(x)
+            np.testing.assert_allclose(mat, exp, atol=1e-8, err_msg=w.name)
+            np.testing.assert_allclose(t.recompose(mat), x, atol=1e-8, err_msg=w.name)
+            for lev in range(mat.shape[0]):
+                np.testing.assert_allclose(t.recompose(mat, lev), x, atol=1e-8, err_msg=w.name)
+    with pytest.raises(jw.JWaveFailure, match="calcExponent"):
+        jw.FastWaveletTransform(jw.by_class("Haar1"), ctx).decompose(np.ones(12))
+
+
+# ------------------------------------------------------- flattened MODWT API
+def test_modwt_flattened_interface(ctx):
+    """MODWT1DInterfaceTest (MODWT1DInterfaceTest.java:22-136) through the
+    native path, plus bit-exactness vs the oracle: forward(x) / forward(x,
+    level) flatten [W_1..W_J, V_J]; reverse(flat, level) and the auto-level
+    reverse(flat) (MODWTTransform.java:389-443, 854-912)."""
+    haar, d4 = jw.by_class("Haar1"), jw.by_class("Daubechies4")
+    m = jw.MODWTTransform(haar, ctx)
+    sig8 = np.arange(1.0, 9.0)
+    flat = m.forward(sig8)
+    assert flat.shape == (8 * 4,)
+    assert_exact(flat, oracle.modwt_forward(haar, sig8, 3).reshape(-1), "flat fwd")
+    assert_exact(m.reverse(flat), oracle.modwt_inverse(haar, flat.reshape(4, 8)), "auto rev")
+    np.testing.assert_allclose(m.reverse(flat), sig8, atol=1e-10)
+    sig64 = np.sin(2 * np.pi * np.arange(64) / 16.0)
+    for level in range(1, 7):
+        f = m.forward(sig64, level)
+        assert f.shape == (64 * (level + 1),)
+        assert_exact(f, oracle.modwt_forward(haar, sig64, level).reshape(-1), "lvl %d" % level)
+    md = jw.MODWTTransform(d4, ctx)
+    sig128 = np.cos(2 * np.pi * np.arange(128) / 32.0) + 0.5 * np.sin(2 * np.pi * np.arange(128) / 8.0)
+    for level in range(1, 6):
+        f = md.forward(sig128, level)
+        r = md.reverse(f, level)
+        assert_exact(r, oracle.modwt_inverse(d4, f.reshape(level + 1, 128)), "rev lvl %d" % level)
+        np.testing.assert_allclose(r, sig128, atol=1e-10)
+    c2 = m.forwardMODWT(sig8, 2)
+    assert_exact(m.forward(sig8, 2), np.asarray(c2).reshape(-1), "1D vs 2D interface")
+    # the reference's ambiguous auto-level guess is reproduced: N=16, J=1 reads as N=8, J=3
+    sig16 = rnd(16, seed=2)
+    f16 = m.forward(sig16, 1)
+    assert_exact(m.reverse(f16), oracle.modwt_inverse(haar, f16.reshape(4, 8)), "ambiguous")
+    with pytest.raises(jw.JWaveFailure, match="2\\^p"):
+        m.forward(np.zeros(10))
+    with pytest.raises(jw.JWaveFailure, match="out of range"):
+        m.forward(np.zeros(8), 5)
+    with pytest.raises(jw.JWaveFailure, match="does not match|Invalid coefficient array"):
+        m.reverse(np.zeros(15), 2)
+    assert m.forward(np.zeros(0)).shape == (0,) and m.reverse(np.zeros(0)).shape == (0,)
+
+
+def test_modwt_flattened_device_tensors(ctx):
+    import torch
+    d4 = jw.by_class("Daubechies4")
+    md = jw.MODWTTransform(d4, ctx)
+    x = rnd(256, seed=9)
+    xd = torch.from_numpy(x).cuda()
+    f = md.forward(xd, 4)
+    assert isinstance(f, torch.Tensor) and f.is_cuda and f.shape == (5 * 256,)
+    assert_exact(f.cpu().numpy(), oracle.modwt_forward(d4, x, 4).reshape(-1), "dev flat fwd")
+    r = md.reverse(f)  # auto: 1280 = 256 x 5 -> first fit N=256, J=4
+    assert isinstance(r, torch.Tensor)
+    assert_exact(r.cpu().numpy(), oracle.modwt_inverse(d4, oracle.modwt_forward(d4, x, 4)), "dev auto")
+
+
+# ------------------------------------------------------------- reentrancy
+def test_c_abi_reentrancy_threads():
+    """Every C-ABI entry is reentrant: two threads with a context
+    each, and two threads sharing one context (its mutex serialises them),
+    hammer FWT / WPT / MODWT concurrently — the pattern of
+    MODWTThreadSafetyTest.java:24-148 — and every result stays bit-exact."""
+    import threading
+    d4, s8 = jw.by_class("Daubechies4"), jw.by_class("Symlet8")
+    x = rnd(1 << 14, seed=21)
+    refs = {"fwt": oracle.fwt_forward(d4, x, 14), "wpt": oracle.wpt_forward(s8, x, 5),
+            "modwt": oracle.modwt_forward(d4, x[:5000], 6)}
+    shared = jw.Context(0, "exact")
+    own = [jw.Context(0, "exact") for _ in range(2)]
+    errors = []
+
+    def worker(c, i):
+        try:
+            for k in range(12):
+                op = ("fwt", "wpt", "modwt")[(i + k) % 3]
+                if op == "fwt":
+                    got = T.fwt_forward(x, d4, 14, c)
+                elif op == "wpt":
+                    got = T.wpt_forward(x, s8, 5, c)
+                else:
+                    got = T.modwt_forward(x[:5000], d4, 6, c)
+                if not np.array_equal(np.asarray(got), refs[op]):
+                    errors.append("%s thread %d iter %d" % (op, i, k))
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=worker, args=(own[0], 0)),
+           threading.Thread(target=worker, args=(own[1], 1)),
+           threading.Thread(target=worker, args=(shared, 2)),
+           threading.Thread(target=worker, args=(shared, 3))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=120)
+    for c in own + [shared]:
+        c.close()
+    assert not errors, errors[:5]
 
 
 def test_complex_entry(ctx):

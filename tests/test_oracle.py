@@ -103,6 +103,59 @@ def test_stepping_kat(w):
             np.testing.assert_allclose(oracle.wpt_reverse(w, yw, p), x, atol=1e-8)
 
 
+def _decompose_oracle(w, x):
+    """WaveletTransform.decompose (WaveletTransform.java:136-145) on the oracle:
+    row p = forward(x, p), p = 0..log2 n."""
+    return np.stack([oracle.fwt_forward(w, x, p) for p in range(len(x).bit_length())])
+
+
+@pytest.mark.parametrize("w", CREATE2ARR, ids=lambda w: w.name)
+def test_decompose_kat(w):
+    """DecomposeTest.testDecompose (DecomposeTest.java:30-170): constant
+    signals of 4 and 64 give the orthonormal pyramid (row p: 2^(p/2) in the
+    first n/2^p slots), delta 1e-8; recompose (WaveletTransform.java:173-182:
+    reverse(row level, level)) from every level returns the signal."""
+    for n in (4, 64):
+        x = np.ones(n)
+        mat = _decompose_oracle(w, x)
+        exp = np.stack([_stepping_expect(n, p) for p in range(n.bit_length())])
+        np.testing.assert_allclose(mat, exp, atol=1e-8)
+        for lev in range(mat.shape[0]):
+            np.testing.assert_allclose(oracle.fwt_reverse(w, mat[lev], lev), x, atol=1e-8)
+
+
+def test_modwt_flattened_host_logic(monkeypatch):
+    """MODWTTransform's flattened API host logic (MODWTTransform.java:389-443,
+    854-912) without a device: validation messages, and the auto-level
+    reverse(double[]) search — the first N = 2^p with total/N - 1 <= p,
+    including the reference's ambiguity (N=16, J=1 is read as N=8, J=3)."""
+    m = jw.MODWTTransform(jw.by_class("Haar1"))
+    seen = []
+    monkeypatch.setattr(m, "inverseMODWT", lambda c: seen.append(np.asarray(c).shape) or "ok")
+    assert m.reverse(np.zeros(32)) == "ok" and seen[-1] == (4, 8)      # N=8, J=3
+    assert m.reverse(np.zeros(16 * 2)) == "ok" and seen[-1] == (4, 8)  # N=16,J=1 -> N=8,J=3
+    assert m.reverse(np.zeros(1024 * 5)) == "ok" and seen[-1] == (10, 512)  # 512 x 10 fits first
+    assert m.reverse(np.zeros(2)) == "ok" and seen[-1] == (1, 2)       # N=2, J=0
+    with pytest.raises(jw.JWaveFailure, match="Cannot determine original signal dimensions"):
+        m.reverse(np.zeros(7))
+    with pytest.raises(jw.JWaveFailure, match="Invalid coefficient array for given level"):
+        m.reverse(np.zeros(15), 2)
+    with pytest.raises(jw.JWaveFailure, match="does not match expected size"):
+        m.reverse(np.zeros(17), 1)
+    with pytest.raises(jw.JWaveFailure, match="calcExponent"):
+        m.forward(np.zeros(10))
+    with pytest.raises(jw.JWaveFailure, match=r"MODWTTransform#forward - given array length"):
+        m.forward(np.zeros(10), 2)
+    with pytest.raises(jw.JWaveFailure, match="out of range"):
+        m.forward(np.zeros(8), 5)
+    with pytest.raises(jw.JWaveFailure, match="maximum supported decomposition level is 13"):
+        m.forward(np.zeros(1 << 14), 14)
+    with pytest.raises(ValueError, match="maximum supported decomposition level is 13"):
+        m.forward(np.zeros(1 << 14))  # full depth 14 > 13: forwardMODWT's IllegalArgumentException
+    with pytest.raises(ValueError, match="at least 1"):
+        m.forward(np.zeros(8), 0)
+
+
 @pytest.mark.parametrize("w", CREATE2ARR[:20] + CREATE2ARR[25:32], ids=lambda w: w.name)
 def test_general_roundtrip(w):
     """GeneralTest.testExample (GeneralTest.java:36-80): fixed 8-vector round trip."""
