@@ -11,7 +11,9 @@ import threading
 from .exceptions import JWaveError
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libjwave_hip.so")
+# JWAVE_AMD_LIB: an alternative build of the same library (tools/sanitize.sh
+# points it at the ASan/UBSan host build); default: the in-tree build.
+LIB_PATH = os.environ.get("JWAVE_AMD_LIB") or os.path.join(HERE, "lib", "libjwave_hip.so")
 HEADER = os.path.join(HERE, "..", "include", "jwave_hip.h")
 
 JWV_OK = 0
@@ -141,7 +143,7 @@ def lib(path=None):
             import torch  # noqa: F401
         except ImportError:
             pass
-        if os.environ.get("JWAVE_AMD_NO_BUILD") != "1":
+        if os.environ.get("JWAVE_AMD_NO_BUILD") != "1" and not os.environ.get("JWAVE_AMD_LIB"):
             try:
                 from . import _build
                 if _build.stale():

@@ -34,8 +34,10 @@ def build(force=False):
 def lib():
     global _lib
     if _lib is None:
-        build()
-        _lib = ctypes.CDLL(_LIB_PATH)
+        alt = os.environ.get("JWAVE_ORACLE_LIB")  # tools/sanitize.sh: ASan/UBSan build
+        if not alt:
+            build()
+        _lib = ctypes.CDLL(alt or _LIB_PATH)
         i64, c_int = ctypes.c_int64, ctypes.c_int
         tp = ctypes.POINTER(_Taps)
         for name in ("orc_fwt_forward", "orc_fwt_reverse", "orc_wpt_forward", "orc_wpt_reverse"):
