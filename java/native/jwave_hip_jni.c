@@ -173,3 +173,36 @@ JNIEXPORT jint JNICALL Java_jwave_amd_HipNative_modwt(
   unpin_all(&P);
   return rc;
 }
+
+/* AncientEgyptianDecomposition(FWT | WPT).forward|reverse(double[]) of any
+ * length: one call, the small pieces in one varlen launch (jwv_aed_*) */
+JNIEXPORT jint JNICALL Java_jwave_amd_HipNative_aed(
+    JNIEnv* env, jclass cls, jlong ctx, jint kind, jboolean fwd, jdoubleArray jx, jdoubleArray jy,
+    jint L, jint tw, jdouble scale, jdoubleArray jlo, jdoubleArray jhi, jdoubleArray jlor,
+    jdoubleArray jhir) {
+  const jsize n = (*env)->GetArrayLength(env, jx);
+  pins P = {env, {0}, {0}, {0}, 0};
+  PIN_TAPS(P);
+  const double* x = pin(&P, jx, JNI_ABORT);
+  double* y = pin(&P, jy, 0);
+  const int rc = fwd ? jwv_aed_fwd_f64(x, y, n, kind, &t, CTX(ctx))
+                     : jwv_aed_rev_f64(x, y, n, kind, &t, CTX(ctx));
+  unpin_all(&P);
+  return rc;
+}
+
+/* WaveletTransform.decompose(double[]): mat = (log2 n + 1) * n, row p =
+ * forward(x, p) (jwv_decompose_f64) */
+JNIEXPORT jint JNICALL Java_jwave_amd_HipNative_decompose(
+    JNIEnv* env, jclass cls, jlong ctx, jint kind, jdoubleArray jx, jdoubleArray jmat, jint L,
+    jint tw, jdouble scale, jdoubleArray jlo, jdoubleArray jhi, jdoubleArray jlor,
+    jdoubleArray jhir) {
+  const jsize n = (*env)->GetArrayLength(env, jx);
+  pins P = {env, {0}, {0}, {0}, 0};
+  PIN_TAPS(P);
+  const double* x = pin(&P, jx, JNI_ABORT);
+  double* mat = pin(&P, jmat, 0);
+  const int rc = jwv_decompose_f64(x, mat, n, kind, &t, CTX(ctx));
+  unpin_all(&P);
+  return rc;
+}

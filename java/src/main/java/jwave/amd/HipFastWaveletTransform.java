@@ -48,6 +48,28 @@ public class HipFastWaveletTransform extends FastWaveletTransform {
     return out;
   }
 
+  /**
+   * WaveletTransform.decompose (WaveletTransform.java:136-145) in ONE native
+   * call: row p = forward(arrTime, p) for p = 0..log2 n (jwv_decompose_f64).
+   * recompose(m, level) is the inherited reverse(m[level], level) (:173-182).
+   */
+  @Override public double[ ][ ] decompose( double[ ] arrTime ) throws JWaveException {
+    if( _taps == null )
+      return super.decompose( arrTime );
+    int n = arrTime.length;
+    int rows = 32 - Integer.numberOfLeadingZeros( Math.max( n, 1 ) );  // log2 n + 1 for 2^p
+    double[ ] mat = new double[ rows * n ];
+    HipNative.Taps t = _taps;
+    HipNative.check( HipNative.decompose( HipNative.ctx( ), _kind, arrTime, mat, t.L, t.tw,
+        t.scale, t.lo, t.hi, t.loR, t.hiR ) );
+    return HipNative.unpack( mat, rows, n );
+  }
+
+  /** The bank this transform sends to the GPU, or null (Java fallback). */
+  HipNative.Taps taps( ) { return _taps; }
+
+  int kind( ) { return _kind; }
+
   @Override public double[ ][ ] forward( double[ ][ ] m, int lvlM, int lvlN )
       throws JWaveException {
     if( _taps == null )

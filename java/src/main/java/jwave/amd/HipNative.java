@@ -115,6 +115,14 @@ public final class HipNative {
   static native int modwt( long ctx, boolean forward, double[ ] x, double[ ] wv, int n, int J,
       int L, int tw, double[ ] lo, double[ ] hi, double[ ] loR, double[ ] hiR );
 
+  /** AncientEgyptianDecomposition over FWT (kind 0) / WPT (kind 1), any length. */
+  static native int aed( long ctx, int kind, boolean forward, double[ ] x, double[ ] y, int L,
+      int tw, double scale, double[ ] lo, double[ ] hi, double[ ] loR, double[ ] hiR );
+
+  /** mat = (log2 n + 1) * n doubles, row p = forward(x, p). */
+  static native int decompose( long ctx, int kind, double[ ] x, double[ ] mat, int L, int tw,
+      double scale, double[ ] lo, double[ ] hi, double[ ] loR, double[ ] hiR );
+
   static int t1( int kind, boolean fwd, double[ ] x, double[ ] y, int level, Taps t ) {
     return transform1d( ctx( ), kind, fwd, x, y, level, t.L, t.tw, t.scale, t.lo, t.hi, t.loR,
         t.hiR );

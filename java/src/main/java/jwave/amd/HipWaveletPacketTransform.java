@@ -33,6 +33,22 @@ public class HipWaveletPacketTransform extends WaveletPacketTransform {
     return out;
   }
 
+  /** WaveletTransform.decompose (WaveletTransform.java:136-145) for the packet
+   *  tree in ONE native call: row p = forward(arrTime, p). */
+  @Override public double[ ][ ] decompose( double[ ] arrTime ) throws JWaveException {
+    if( _taps == null )
+      return super.decompose( arrTime );
+    int n = arrTime.length;
+    int rows = 32 - Integer.numberOfLeadingZeros( Math.max( n, 1 ) );
+    double[ ] mat = new double[ rows * n ];
+    HipNative.Taps t = _taps;
+    HipNative.check( HipNative.decompose( HipNative.ctx( ), 1, arrTime, mat, t.L, t.tw, t.scale,
+        t.lo, t.hi, t.loR, t.hiR ) );
+    return HipNative.unpack( mat, rows, n );
+  }
+
+  HipNative.Taps taps( ) { return _taps; }
+
   /** Every row (one signal each, equal lengths) with the same level: one
    *  native call instead of one per signal. */
   public double[ ][ ] forwardBatch( double[ ][ ] signals, int level ) throws JWaveException {
