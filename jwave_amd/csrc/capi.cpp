@@ -935,6 +935,10 @@ bool Geo::fwt1() {
   static const bool p = env_int("JWV_FWT1", 1) != 0;
   return p;
 }
+int Geo::slab_order() {
+  static const int o = env_int("JWV_SLAB_ORDER", 1) ? 1 : 0;
+  return o;
+}
 int Geo::store_pol() {
   static const int p = env_int("JWV_STPOL", 0);
   return p < 0 || p > 2 ? 0 : p;

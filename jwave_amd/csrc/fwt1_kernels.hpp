@@ -152,56 +152,128 @@ struct Rev1Geo {
   static constexpr int dtotal() { return doff(-1); }
   static constexpr int buf1() { return dtotal(); }
   static constexpr int buf0() { return dtotal() + len(1); }
+  // + 4: a couple of Rev1Level reads up to 3 values past its window
   static constexpr int lds_doubles() {
-    return dtotal() + len(1) + (K >= 2 ? (len(2) > len(K) ? len(2) : len(K)) : 0);
+    return dtotal() + len(1) + (K >= 2 ? (len(2) > len(K) ? len(2) : len(K)) : 0) + 4;
   }
   static_assert(((T >> K) & 1) == 0, "T/2^K must be even");
 };
 
-template <int L, int NT, int T, int K, bool FMA, int l, bool WT = false>
+// Each lane synthesises two adjacent pairs (ml, ml+1) of one level ("a
+// couple"): they share Q-1 of their Q a/d inputs, so the lane reads Q+1 (+1
+// for alignment) values per operand with 16-B LDS reads at a 16-B lane stride
+// (conflict-free), instead of 2Q 8-B reads per pair.
+#ifndef JWV_REV_COUPLE0
+#define JWV_REV_COUPLE0 0
+#endif
+template <int L, int NT, int T, int K, bool FMA, int l, bool WT = false, bool CP = false>
 struct Rev1Level {
   __device__ __forceinline__ static void run(const RevTaps<L>& tp, double* lds, int t,
                                              double* __restrict__ y, int sp = 0) {
     using G = Rev1Geo<L, T, K>;
     JWV_STAMP(20 + l);
     constexpr int Q = G::Q;
-    constexpr int np = G::len(l) / 2;                    // pairs of this level's window
-    constexpr int off = G::c(l + 1) - G::c(l) / 2;       // local index of a[pair 0]
-    constexpr int R = (np + NT - 1) / NT;
+    constexpr int np = G::len(l) / 2;               // pairs of this level's window
+    constexpr int NC = (np + 1) / 2;                // couples
+    constexpr int off = G::c(l + 1) - G::c(l) / 2;  // local index of a[pair 0]
+    constexpr int sh = (off - (Q - 1)) & 1;         // 1: reads start one lower (even)
+    constexpr int NR = (Q + 3) & ~1;                // values read per operand (even, >= Q+2)
+    constexpr int R = (NC + NT - 1) / NT;
+    constexpr int RS = (np + NT - 1) / NT;
+    // CP: couples (throughput-bound tile passes; the latency-bound head and
+    // chain kernels keep one pair per lane: twice the lanes per level).
+    // Level 0 stores to global memory: one pair per lane keeps those stores
+    // contiguous (a couple's two 16-B stores at a 32-B lane stride cost the
+    // HBM-bound passes more than the LDS reads they save).
+    // Short banks (L <= 8: 2Q <= 8 reads per pair) measured slower with
+    // couples on the HBM-bound 1D pass (config 2, +1.7 us/step); L = 16 rows
+    // of config 3 gain 11% on the reverse tile.
+    constexpr bool kCouple = CP && L >= 12 && (l > 0 || JWV_REV_COUPLE0);
+    static_assert(Q - 2 + G::c(l) / 2 < NT, "array-head pairs must sit in slot 0");
     const double* ab = lds + ((((l + 1) & 1) != 0) ? G::buf1() : G::buf0());
     const double* db = lds + G::doff(l);
     double* ob = lds + (((l & 1) != 0) ? G::buf1() : G::buf0());
     const int tid = opaque_tid();  // per-level: keeps address math out of the prologue
+    const int pbase = t * (T >> (l + 1)) - G::c(l) / 2;  // global index of window pair 0
+    auto is_head = [&](int ml) { return pbase + ml >= 0 && pbase + ml < Q - 1; };
+    auto put = [&](int ml, double xe, double xo, bool w) {
+      if (!w) return;
+      if constexpr (l == 0) {  // WT: handed to another workgroup of this launch
+        if constexpr (WT) st2<true>(y + (int64_t)t * T + 2 * ml, xe, xo);
+        else st2_pol(y + (int64_t)t * T, 2 * ml, xe, xo, sp);
+      } else {
+        *reinterpret_cast<double2*>(ob + 2 * ml) = make_double2(xe, xo);
+      }
+    };
+    if constexpr (kCouple) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int ml = tid + r * NT;
-      if ((r + 1) * NT <= np || ml < np) {
+      for (int r = 0; r < R; ++r) {
+        const int k = tid + r * NT;
+        if ((r + 1) * NT <= NC || k < NC) {
+          const int ml = 2 * k;
+          const int st = off + ml - (Q - 1) - sh;  // even
+          double av[NR], dv[NR];
+#pragma unroll
+          for (int j = 0; j < NR; j += 2) {
+            const double2 u = *reinterpret_cast<const double2*>(ab + st + j);
+            const double2 w = *reinterpret_cast<const double2*>(db + st + j);
+            av[j] = u.x;
+            av[j + 1] = u.y;
+            dv[j] = w.x;
+            dv[j + 1] = w.y;
+          }
+          // pair ml reads a[li - q] = av[(Q-1) + sh - q]; pair ml+1 one further
+          double x0e, x0o, x1e, x1o;
+          rev_pair<L, FMA>(tp, av + (Q - 1) + sh, dv + (Q - 1) + sh, 1, x0e, x0o);
+          rev_pair<L, FMA>(tp, av + Q + sh, dv + Q + sh, 1, x1e, x1o);
+          // array-head pairs are left to the fix-up below (block-uniform test)
+          bool w0 = true, w1 = (np % 2 == 0) || ml + 1 < np;  // odd np: last couple single
+          if (r == 0 && pbase < Q - 1) {
+            w0 = !is_head(ml);
+            w1 = w1 && !is_head(ml + 1);
+          }
+          put(ml, x0e, x0o, w0);
+          put(ml + 1, x1e, x1o, w1);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < RS; ++r) {
+        const int ml = tid + r * NT;
+        if ((r + 1) * NT <= np || ml < np) {
+          const int li = off + ml;
+          double xe, xo;
+          // array-head tiles (block-uniform): the rotated form for every pair
+          // of the slot, r = Q-1 (the interior order) for non-head pairs
+          if (r == 0 && pbase < Q - 1) {
+            const int mg = pbase + ml;
+            rev_pair_rot<L, FMA>(tp, [=](int q) { return ab[li - q]; },
+                                 [=](int q) { return db[li - q]; }, is_head(ml) ? mg : Q - 1,
+                                 xe, xo);
+          } else {
+            rev_pair<L, FMA>(tp, ab + li, db + li, 1, xe, xo);
+          }
+          put(ml, xe, xo, true);
+        }
+      }
+    }
+    // Couples: array-head pairs (global pair index mg < Q-1,
+    // Wavelet.java:284-296 order = the interior order rotated, rev_pair_rot)
+    // only in the first tiles of a row, one lane each, after the interior pass
+    // so the rotation's registers are never live beside a couple's.
+    if (kCouple && pbase < Q - 1 && tid < Q - 1) {
+      const int ml = tid - pbase;
+      if (ml >= 0 && ml < np) {
         const int li = off + ml;
         double xe, xo;
-        // array-head pairs (global pair index in [0, Q-1)): in tile 0, and in
-        // the halo of the next tiles at deep levels where c_l > T/2^l.  The
-        // window's first global pair pbase decides for the whole block; those
-        // blocks take the rotated form for every pair of the slot (one path).
-        const int pbase = t * (T >> (l + 1)) - G::c(l) / 2;
-        if (r == 0 && pbase < Q - 1) {
-          const int mg = pbase + ml;
-          rev_pair_rot<L, FMA>(tp, [=](int q) { return ab[li - q]; },
-                               [=](int q) { return db[li - q]; },
-                               (mg >= 0 && mg < Q - 1) ? mg : Q - 1, xe, xo);
-        } else {
-          rev_pair<L, FMA>(tp, ab + li, db + li, 1, xe, xo);
-        }
-        if constexpr (l == 0) {  // WT: handed to another workgroup of this launch
-          if constexpr (WT) st2<true>(y + (int64_t)t * T + 2 * ml, xe, xo);
-          else st2_pol(y + (int64_t)t * T, 2 * ml, xe, xo, sp);
-        } else {
-          *reinterpret_cast<double2*>(ob + 2 * ml) = make_double2(xe, xo);
-        }
+        rev_pair_rot<L, FMA>(tp, [=](int q) { return ab[li - q]; },
+                             [=](int q) { return db[li - q]; }, tid, xe, xo);
+        put(ml, xe, xo, true);
       }
     }
     if constexpr (l > 0) {
       lds_barrier();
-      Rev1Level<L, NT, T, K, FMA, l - 1, WT>::run(tp, lds, t, y, sp);
+      Rev1Level<L, NT, T, K, FMA, l - 1, WT, CP>::run(tp, lds, t, y, sp);
     }
   }
 };
@@ -241,7 +313,7 @@ __global__ __launch_bounds__(NT) void fwt_rev_tile1(const double* __restrict__ a
                              [&](int e) { return (int64_t)half + ((B + e) & hm); });
   }
   dma_fence_barrier();
-  Rev1Level<L, NT, T, K, FMA, K - 1>::run(tp, lds, t, dst + o * s_d, sp);
+  Rev1Level<L, NT, T, K, FMA, K - 1, false, true>::run(tp, lds, t, dst + o * s_d, sp);
 }
 
 }  // namespace jwv

@@ -49,50 +49,6 @@ __device__ __forceinline__ void rev_pair_wrap(const RevTaps<L>& tp, const double
   pin2(xe, xo);
 }
 
-// Levels with h < L wrap several times: Wavelet.reverse's scatter order
-// (i ascending, j ascending) for all H outputs at once, H a compile-time
-// level size, so every term lands in a fixed register (no per-term test; each
-// output is a chain of L/2 adds).  av/dv: the level's a and d values.
-template <int L, bool FMA, int H>
-__device__ __forceinline__ void rev_small_all(const RevTaps<L>& tp, const double* av,
-                                              const double* dv, double (&x)[H]) {
-#pragma unroll
-  for (int k = 0; k < H; ++k) x[k] = 0.0;
-#pragma unroll
-  for (int i = 0; i < H / 2; ++i)
-#pragma unroll
-    for (int j = 0; j < L; ++j) {
-      double t = av[i] * tp.lo_r[j];
-      t = mac<FMA>(t, dv[i], tp.hi_r[j]);
-      x[(2 * i + j) & (H - 1)] += t;
-    }
-}
-// Output pair (2m, 2m+1) of a level of size H < L.
-template <int L, bool FMA, int H>
-__device__ __forceinline__ void rev_small_pair(const RevTaps<L>& tp, const double* av,
-                                               const double* dv, int m, double& xe, double& xo) {
-  double x[H];
-  rev_small_all<L, FMA, H>(tp, av, dv, x);
-  xe = x[0];
-  xo = x[1];
-#pragma unroll
-  for (int q = 1; q < H / 2; ++q)
-    if (m == q) {
-      xe = x[2 * q];
-      xo = x[2 * q + 1];
-    }
-}
-template <int L, bool FMA>
-__device__ __forceinline__ void rev_small_regs(const RevTaps<L>& tp, const double* av,
-                                               const double* dv, int h, int m, double& xe,
-                                               double& xo) {
-  if constexpr (L > 2) if (h == 2) return rev_small_pair<L, FMA, 2>(tp, av, dv, m, xe, xo);
-  if constexpr (L > 4) if (h == 4) return rev_small_pair<L, FMA, 4>(tp, av, dv, m, xe, xo);
-  if constexpr (L > 8) if (h == 8) return rev_small_pair<L, FMA, 8>(tp, av, dv, m, xe, xo);
-  if constexpr (L > 16) if (h == 16) return rev_small_pair<L, FMA, 16>(tp, av, dv, m, xe, xo);
-  xe = xo = 0.0;  // unreachable: h < L, both powers of two
-}
-
 // ====================================================================
 // Forward, resident, C = 1.  src row: level input of length h0 (DMA-able);
 // dst row: coefficient array (details of level size h at dst[h/2, h), final
@@ -213,7 +169,7 @@ __device__ __forceinline__ void rev_res1_levels(double* lds, int h0, int nlev,
             av[i] = i < half ? lds[i] : 0.0;
             dv[i] = i < half ? lds[half + i] : 0.0;
           }
-          rev_small_regs<L, FMA>(tp, av, dv, hh, m, xe, xo);
+          rev_small_c<L, FMA>(tp, av, dv, 1, hh, m, xe, xo);  // h < L: compile-time h
         } else {
           rev_pair_wrap<L, FMA>(tp, lds, half, m, xe, xo);
         }

@@ -126,15 +126,19 @@ template <int L, int NT, int T, int K, bool FMA>
 __global__ __launch_bounds__(NT) void fwt_fwd_tile8(const double* __restrict__ src, AxisView sv,
                                                     double* __restrict__ dst, AxisView dv,
                                                     double* __restrict__ adst, AxisView av_, int h,
-                                                    int inner, FwdTaps<L> tp) {
+                                                    int inner, FwdTaps<L> tp, int order) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   using G = Fwd1Geo<L, T, K>;
   const int ntile = h / T, ncb = inner >> 3;
   const int nblk = gridDim.x;
   int b = blockIdx.x;
   if ((nblk & 7) == 0) b = (b & 7) * (nblk >> 3) + (b >> 3);
-  const int t = b % ntile;
-  const int rest = b / ntile;
+  // order 0: tile-fastest (a slab's tiles run side by side: halo rows in the
+  // same L2); order 1: slab-fastest (concurrent blocks cover whole matrix
+  // rows: contiguous DRAM rows, both 64-B halves of each 128-B line at once)
+  const int nsl = nblk / ntile;
+  const int t = order ? b / nsl : b % ntile;
+  const int rest = order ? b % nsl : b / ntile;
   const int64_t o = rest / ncb;
   const int c0 = (rest % ncb) * 8;
   const double* s = src + view_base(sv, o) + c0;
@@ -213,15 +217,19 @@ template <int L, int NT, int T, int K, bool FMA>
 __global__ __launch_bounds__(NT) void fwt_rev_tile8(const double* __restrict__ asrc, AxisView as,
                                                     const double* __restrict__ coef, AxisView cv,
                                                     double* __restrict__ dst, AxisView dv, int hK,
-                                                    int inner, RevTaps<L> tp) {
+                                                    int inner, RevTaps<L> tp, int order) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   using G = Rev1Geo<L, T, K>;
   const int ntile = hK / T, ncb = inner >> 3;
   const int nblk = gridDim.x;
   int b = blockIdx.x;
   if ((nblk & 7) == 0) b = (b & 7) * (nblk >> 3) + (b >> 3);
-  const int t = b % ntile;
-  const int rest = b / ntile;
+  // order 0: tile-fastest (a slab's tiles run side by side: halo rows in the
+  // same L2); order 1: slab-fastest (concurrent blocks cover whole matrix
+  // rows: contiguous DRAM rows, both 64-B halves of each 128-B line at once)
+  const int nsl = nblk / ntile;
+  const int t = order ? b / nsl : b % ntile;
+  const int rest = order ? b % nsl : b / ntile;
   const int64_t o = rest / ncb;
   const int c0 = (rest % ncb) * 8;
   const double* sa = asrc + view_base(as, o) + c0;

@@ -225,6 +225,46 @@ __device__ double rev_small(const typename FB<L>::Rev& tp, const double* a, cons
   return x;
 }
 
+// rev_small for compiled-in banks: all H outputs of a level of size H < L at
+// compile-time H (Wavelet.reverse's scatter order, i then j ascending, each
+// output a fixed chain), then the pair (2m, 2m+1) by register select.  A, D:
+// the level's a and d values at stride `stride`.
+template <int L, bool FMA, int H>
+__device__ __forceinline__ void rev_small_cH(const RevTaps<L>& tp, const double* A,
+                                             const double* D, int stride, int m, double& xe,
+                                             double& xo) {
+  double x[H];
+#pragma unroll
+  for (int k = 0; k < H; ++k) x[k] = 0.0;
+#pragma unroll
+  for (int i = 0; i < H / 2; ++i) {
+    const double a = A[i * stride], d = D[i * stride];
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      double t = a * tp.lo_r[j];
+      t = mac<FMA>(t, d, tp.hi_r[j]);
+      x[(2 * i + j) & (H - 1)] += t;
+    }
+  }
+  xe = x[0];
+  xo = x[1];
+#pragma unroll
+  for (int q = 1; q < H / 2; ++q)
+    if (m == q) {
+      xe = x[2 * q];
+      xo = x[2 * q + 1];
+    }
+}
+template <int L, bool FMA>
+__device__ __forceinline__ void rev_small_c(const RevTaps<L>& tp, const double* A, const double* D,
+                                            int stride, int h, int m, double& xe, double& xo) {
+  if constexpr (L > 2) if (h == 2) return rev_small_cH<L, FMA, 2>(tp, A, D, stride, m, xe, xo);
+  if constexpr (L > 4) if (h == 4) return rev_small_cH<L, FMA, 4>(tp, A, D, stride, m, xe, xo);
+  if constexpr (L > 8) if (h == 8) return rev_small_cH<L, FMA, 8>(tp, A, D, stride, m, xe, xo);
+  if constexpr (L > 16) if (h == 16) return rev_small_cH<L, FMA, 16>(tp, A, D, stride, m, xe, xo);
+  xe = xo = 0.0;  // unreachable: h < L, both powers of two
+}
+
 // ====================================================================
 // Forward, resident.  Grid: one block per (outer o, column slab cb).
 // src: level input of length h0 (view sv); dst: coefficient array (view dv):
@@ -521,23 +561,37 @@ __device__ __forceinline__ void fwt_rev_res_blk(const double* __restrict__ s, Ax
   dma_fence_barrier();
   JWV_STAMP(1);
 
-  // one synthesis pair of a level of size h >= L, from the LDS level image
+  // one synthesis pair of a level of size h >= L, from the LDS level image.
+  // Compiled-in banks: interior and head pairs on one branch-free path
+  // (rev_pair_rot; the head lanes sit in wave 0 at every level).
   auto pair_at = [&](int h, int p, double& xe, double& xo) {
     const int half = h >> 1, hm = half - 1;
     const int m = p / C, c = p % C;
     const double* lb = lds + c;
-    rev_pair_any<L, FMA>(
-        tp, m, qe, lb + m * C, lb + (half + m) * C, C,
-        [=](int q) { return lb[((m - q) & hm) * C]; },
-        [=](int q) { return lb[(half + ((m - q) & hm)) * C]; }, xe, xo);
+    if constexpr (FB<L>::kStatic) {
+      constexpr int Q = L / 2;
+      rev_pair_rot<L, FMA>(tp, [=](int q) { return lb[((m - q) & hm) * C]; },
+                           [=](int q) { return lb[(half + ((m - q) & hm)) * C]; },
+                           m < Q - 1 ? m : Q - 1, xe, xo);
+    } else {
+      rev_pair_any<L, FMA>(
+          tp, m, qe, lb + m * C, lb + (half + m) * C, C,
+          [=](int q) { return lb[((m - q) & hm) * C]; },
+          [=](int q) { return lb[(half + ((m - q) & hm)) * C]; }, xe, xo);
+    }
   };
-  // levels with h < L wrap several times: literal scatter order (one site)
+  // levels with h < L wrap several times: literal scatter order (one site);
+  // compiled-in banks evaluate all h outputs at compile-time h (rev_small_c)
   auto pair_small = [&](int h, int p, double& xe, double& xo) {
     const int half = h >> 1;
     const int m = p / C, c = p % C;
     const double* lb = lds + c;
-    xe = rev_small<L, FMA>(tp, lb, lb + half * C, C, h, 2 * m);
-    xo = rev_small<L, FMA>(tp, lb, lb + half * C, C, h, 2 * m + 1);
+    if constexpr (FB<L>::kStatic) {
+      rev_small_c<L, FMA>(tp, lb, lb + half * C, C, h, m, xe, xo);
+    } else {
+      xe = rev_small<L, FMA>(tp, lb, lb + half * C, C, h, 2 * m);
+      xo = rev_small<L, FMA>(tp, lb, lb + half * C, C, h, 2 * m + 1);
+    }
   };
 
   int h = h0, lev = 0;

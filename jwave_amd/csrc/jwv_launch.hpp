@@ -97,6 +97,9 @@ struct Geo {
   // C = 8 compile-time-geometry column-slab tiles (fwt8_kernels.hpp): env
   // JWV_FWT8 (default 1)
   static bool fwt8();
+  // block order of the C = 8 slab tiles: 0 tile-fastest, 1 slab-fastest
+  // (env JWV_SLAB_ORDER)
+  static int slab_order();
   // st2_pol policy of the passes that write the full-length output (forward:
   // the first tile pass's details; reverse: the last tile pass): env
   // JWV_STPOL (0 plain, 1 sc1, 2 nt)

@@ -173,7 +173,7 @@ hipError_t fwd8_k(const Bank& b, const TileArgs& a, hipStream_t s) {
   for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
   const dim3 grid((unsigned)(a.nouter * (a.inner / 8) * (a.h / kT8)));
   hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a.src, a.sv, a.dst, a.dv, a.adst, a.av, a.h,
-                     a.inner, tp);
+                     a.inner, tp, Geo::slab_order());
   return hipGetLastError();
 }
 template <int L, int K>
@@ -186,7 +186,7 @@ hipError_t rev8_k(const Bank& b, const TileArgs& a, hipStream_t s) {
   const int hK = a.h << (a.K - 1);
   const dim3 grid((unsigned)(a.nouter * (a.inner / 8) * (hK / kT8)));
   hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a.src, a.sv, a.coef, a.cv, a.dst, a.dv, hK,
-                     a.inner, tp);
+                     a.inner, tp, Geo::slab_order());
   return hipGetLastError();
 }
 template <int L>
