@@ -562,17 +562,21 @@ __device__ __forceinline__ void fwt_rev_res_blk(const double* __restrict__ s, Ax
   JWV_STAMP(1);
 
   // one synthesis pair of a level of size h >= L, from the LDS level image.
-  // Compiled-in banks: interior and head pairs on one branch-free path
-  // (rev_pair_rot; the head lanes sit in wave 0 at every level).
+  // Compiled-in banks: interior pairs read without wrapping; the array-head
+  // pairs (m < Q-1, rotated order, rev_pair_rot) sit in wave 0 at every
+  // level, so only wave 0 runs both paths.
   auto pair_at = [&](int h, int p, double& xe, double& xo) {
     const int half = h >> 1, hm = half - 1;
     const int m = p / C, c = p % C;
     const double* lb = lds + c;
     if constexpr (FB<L>::kStatic) {
       constexpr int Q = L / 2;
-      rev_pair_rot<L, FMA>(tp, [=](int q) { return lb[((m - q) & hm) * C]; },
-                           [=](int q) { return lb[(half + ((m - q) & hm)) * C]; },
-                           m < Q - 1 ? m : Q - 1, xe, xo);
+      if (m >= Q - 1) {
+        rev_pair<L, FMA>(tp, lb + m * C, lb + (half + m) * C, C, xe, xo);
+      } else {
+        rev_pair_rot<L, FMA>(tp, [=](int q) { return lb[((m - q) & hm) * C]; },
+                             [=](int q) { return lb[(half + ((m - q) & hm)) * C]; }, m, xe, xo);
+      }
     } else {
       rev_pair_any<L, FMA>(
           tp, m, qe, lb + m * C, lb + (half + m) * C, C,
