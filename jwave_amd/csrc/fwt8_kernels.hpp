@@ -13,8 +13,10 @@
 //    doubles): the 32 lanes of a ds_read_b64 group hold 8 columns x 4 couples
 //    16 rows apart, whose addresses then differ by 136 doubles = 16 banks, so
 //    the group is conflict-free (unpadded, rows 4 apart share all 16 banks:
-//    4-way).  LDS-DMA fills the padded layout directly: one wave instruction
-//    moves 64 x 16 B = 16 rows.  Levels run in place (results wait in
+//    4-way).  A wave's couples share their row phase mod 16, so the window
+//    loads are immediate offsets from one address (item8_couple).  LDS-DMA
+//    fills the padded layout directly: one wave instruction moves 64 x 16 B =
+//    16 rows.  Levels run in place (results wait in
 //    registers across one barrier);
 //  * reverse: one pair per lane, consecutive lanes on consecutive columns then
 //    pairs (a 256-B conflict-free span per 32 lanes); every window of the tile
@@ -29,12 +31,31 @@ namespace jwv {
 // padded LDS row offset (doubles) of window row r
 __host__ __device__ constexpr int prow8(int r) { return 8 * (r + (r >> 4)); }
 
-// forward work item w -> column c = w & 7 and couple q; 128 items = 16
-// couples x 8 columns; the 32 items of one ds_read group sit at couples
-// q0, q0+4, q0+8, q0+12 (rows 16 apart)
+// forward work item w -> column c = w & 7, couple q = 32*qg + 4*qa + qb with
+// qa = (w >> 3) & 7, qb = (w >> 6) & 3 (one value per wave), qg = w >> 8.  The
+// 32 items of one ds_read group sit at couples 4 apart (rows 16 apart: 17
+// padded rows = 136 doubles = 8 banks-of-8-B apart, conflict-free), and since
+// qb is wave-uniform the pad rows a couple's L+2 window crosses are too: the
+// window loads become compile-time offsets from one address (load_couple8).
 __device__ __forceinline__ int item8_couple(int w) {
-  const int qa = (w >> 3) & 3, qb = w >> 5;
-  return ((qb >> 2) << 4) + (qa << 2) + (qb & 3);
+  return ((w >> 8) << 5) + (((w >> 3) & 7) << 2) + ((w >> 6) & 3);
+}
+
+// x[j] = window row 4q + j of column c; xb = lds + 8*(4q + (4q >> 4)) + c with
+// 4q = 16m + 4*QB, so row 4q + j sits (j + ((4*QB + j) >> 4)) padded rows on
+template <int N, int QB>
+__device__ __forceinline__ void load_couple8_qb(const double* xb, double* x) {
+#pragma unroll
+  for (int j = 0; j < N; ++j) x[j] = xb[8 * (j + ((4 * QB + j) >> 4))];
+}
+template <int N>
+__device__ __forceinline__ void load_couple8(const double* xb, int qb, double* x) {
+  switch (__builtin_amdgcn_readfirstlane(qb)) {  // wave-uniform: a scalar branch
+    case 0: load_couple8_qb<N, 0>(xb, x); break;
+    case 1: load_couple8_qb<N, 1>(xb, x); break;
+    case 2: load_couple8_qb<N, 2>(xb, x); break;
+    default: load_couple8_qb<N, 3>(xb, x); break;
+  }
 }
 
 // W rows x 8 columns -> padded LDS rows by LDS-DMA (16 B per lane).
@@ -71,7 +92,8 @@ struct Fwd8Level {
     constexpr int mo = G::m(l);  // even
     constexpr int own = T >> l;  // even
     constexpr int NCQ = mo / 2;  // couples per column
-    constexpr int NI = ((NCQ + 15) / 16) * 128;
+    constexpr int NI = ((NCQ + 31) / 32) * 256;
+    static_assert(NT % 64 == 0, "qb must be wave-uniform");
     constexpr int R = (NI + NT - 1) / NT;
     const int tid = opaque_tid();  // per-level: keeps address math out of the prologue
     double2 av[R];
@@ -81,8 +103,7 @@ struct Fwd8Level {
       const int c = w & 7, q = item8_couple(w);
       if (((r + 1) * NT <= NI || w < NI) && q < NCQ) {
         double x[L + 2];
-#pragma unroll
-        for (int j = 0; j < L + 2; ++j) x[j] = lds[prow8(4 * q + j) + c];
+        load_couple8<L + 2>(lds + prow8(4 * q) + c, (w >> 6) & 3, x);
         double a0, d0, a1, d1;
         fwd_pair<L, FMA>(tp, [&](int j) { return x[j]; }, a0, d0);
         fwd_pair<L, FMA>(tp, [&](int j) { return x[j + 2]; }, a1, d1);
