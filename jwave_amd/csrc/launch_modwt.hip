@@ -53,10 +53,11 @@ int env_variant(const char* name) {
   return v ? std::atoi(v) : -1;
 }
 // Defaults measured on config 5 (D4, J=8, N=1e7): fwd 1 (512 x 4096) 228 ->
-// 203 us, inv 2 (512 x 2048) 386 -> 300 us.  The register-blocked (3-6) and
-// two-deep prefetch (7-9) variants measured no better and stay selectable.
+// 203 us, inv 2 (512 x 2048) 386 -> 300 us, inv 10 (class-major layout, 512 x
+// 2048) 300 -> 285 us.  The register-blocked (3-6) and two-deep prefetch
+// (7-9) variants measured no better and stay selectable.
 int fwd_variant() { static const int v = env_variant("JWV_MODFWD"); return v < 0 ? 1 : v; }
-int inv_variant() { static const int v = env_variant("JWV_MODINV"); return v < 0 ? 2 : v; }
+int inv_variant() { static const int v = env_variant("JWV_MODINV"); return v < 0 ? 10 : v; }
 
 template <int L, int NTX, int TX>
 hipError_t fwd_tile_go(const Bank& b, const ModwtArgs& a, hipStream_t s) {
@@ -149,6 +150,23 @@ hipError_t inv_tile_g_go(const Bank& b, const ModwtArgs& a, hipStream_t s) {
   }
 }
 
+template <int L, int NTX, int TX>
+hipError_t inv_tile_cm_go(const Bank& b, const ModwtArgs& a, hipStream_t s) {
+  if constexpr (L == 0) {
+    return inv_tile_go<L, NT, TI>(b, a, s);
+  } else {
+    const auto tp = mtaps<L>(b);
+    auto k = modwt_inv_tile_cm<L, NTX, TX, SMAX, kFMA>;
+    const int buf = ModCm::buf(TX, b.L, a.j0, a.j1);
+    const size_t lds = (size_t)2 * buf * sizeof(double);
+    if (hipError_t e = prep(k, lds)) return e;
+    const dim3 grid((unsigned)((a.N + TX - 1) / TX));
+    hipLaunchKernelGGL(k, grid, dim3(NTX), lds, s, a.src, a.coef, a.ldw, a.vout, a.N, a.j0,
+                       a.j1, buf, tp);
+    return hipGetLastError();
+  }
+}
+
 template <int L>
 hipError_t inv_go(const Bank& b, bool tiled, const ModwtArgs& a, hipStream_t s) {
   if (tiled) {
@@ -162,6 +180,7 @@ hipError_t inv_go(const Bank& b, bool tiled, const ModwtArgs& a, hipStream_t s) 
       case 7: return inv_tile2_go<L, 512, 2048>(b, a, s);
       case 8: return inv_tile2_go<L, 256, 1024>(b, a, s);
       case 9: return inv_tile2_go<L, 1024, 4096>(b, a, s);
+      case 10: return inv_tile_cm_go<L, 512, 2048>(b, a, s);
       default: return inv_tile_go<L, NT, TI>(b, a, s);
     }
   }

@@ -489,4 +489,162 @@ __global__ __launch_bounds__(NT) void modwt_inv_tile_g(const double* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------
+// Inverse tile in class-major ("polyphase") LDS layout (compile-time L).
+// At level j the taps of output p sit st = 2^(j-1) apart, so each residue
+// class r = p mod st is an ordinary stride-1 convolution over m = p div st.
+// Both windows of level j (V_j and W_j) are stored class by class: position
+// q -> r*M_j + m, so a lane's taps are consecutive doubles at immediate
+// offsets for every level (no per-tap address math, no per-level code), and a
+// lane computes two outputs m = 2mb, 2mb+1 of one class from L+2 values read
+// as (L+2)/2 16-B LDS reads.  Lanes walk classes fastest (u -> r = u mod st,
+// mb = u div st) and M_j is padded so that each 16-lane phase of a 16-B read
+// hits 16 distinct 16-B bank groups (M_j/2 odd for st >= 16, M_j/2 = 16/st
+// mod 16 below).  Level j's outputs land directly in level j-1's layout
+// (class r' = r mod st/2, m' = 2m + r div (st/2)).  Same math and order as
+// modwt_inv_tile: each output sums its L taps of V and of W in ascending order
+// from 0.0, then adds the two sums.
+struct ModCm {
+  // class length of level sh (input window Win, output window Wout)
+  __host__ __device__ static int M(int Win, int Wout, int sh, int L) {
+    const int st = 1 << sh;
+    const int Min = (Win + st - 1) >> sh;
+    const int nmb = (((Wout + st - 1) >> sh) + 1) >> 1;
+    int m = Min > 2 * nmb + L ? Min : 2 * nmb + L;
+    int h = (m + 1) >> 1;
+    if (st >= 16) {
+      h |= 1;
+    } else {
+      const int want = 16 / st;
+      h += ((want - h) % 16 + 16) % 16;
+    }
+    return 2 * h;
+  }
+  __host__ __device__ static int nmb(int Wout, int sh) {
+    return ((((Wout + (1 << sh) - 1) >> sh) + 1) >> 1);
+  }
+  // doubles per buffer over levels j0..j1 (host: LDS size)
+  __host__ static int buf(int T, int L, int j0, int j1) {
+    int b = 0;
+    for (int j = j1; j >= j0; --j) {
+      const int Rj = (L - 1) * ((1 << j) - (1 << (j0 - 1)));
+      const int Rn = Rj - (L - 1) * (1 << (j - 1));
+      const int v = (1 << (j - 1)) * M(T + Rj, T + Rn, j - 1, L);
+      b = v > b ? v : b;
+    }
+    return (b + 1) & ~1;
+  }
+};
+
+template <int L, int NT, int T, int SMAX, bool FMA>
+__global__ __launch_bounds__(NT) void modwt_inv_tile_cm(const double* __restrict__ vsrc,
+                                                        const double* __restrict__ coef,
+                                                        int64_t ldw, double* __restrict__ dst,
+                                                        int64_t N, int j0, int j1, int buf,
+                                                        ModwtTaps<L> tp) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  constexpr int MAXP = (T + SMAX + NT - 1) / NT;
+  constexpr int MAXI = (T + SMAX) / (2 * NT) + 2;  // item slots: nmb*st <= W/2 + st
+  const int R = (L - 1) * ((1 << j1) - (1 << (j0 - 1)));
+  double* vb = lds;
+  double* wb = lds + buf;
+  const int64_t t0 = xcd_tile() * T;
+  const int tid = threadIdx.x;
+  const bool inside = t0 + T + R <= N;  // block-uniform: no wrap
+  auto gidx = [&](int q) { return inside ? t0 + q : wrap_mod(t0 + q, N); };
+  // the next level's W window, in flight in registers during a level
+  double pw[MAXP];
+  auto fetch = [&](const double* row, int W) {
+#pragma unroll
+    for (int r = 0; r < MAXP; ++r) {
+      const int q = tid + r * NT;
+      if (q < W) pw[r] = row[gidx(q)];
+    }
+  };
+  // registers -> class-major layout (sh, class length M)
+  auto scatter = [&](double* b, int W, int sh, int M) {
+    const int msk = (1 << sh) - 1;
+#pragma unroll
+    for (int r = 0; r < MAXP; ++r) {
+      const int q = tid + r * NT;
+      if (q < W) b[(q & msk) * M + (q >> sh)] = pw[r];
+    }
+  };
+  auto halo = [&](int j) { return (L - 1) * ((1 << j) - (1 << (j0 - 1))); };
+  {
+    fetch(vsrc, T + R);
+    const int sh = j1 - 1;
+    scatter(vb, T + R, sh, ModCm::M(T + R, T + halo(j1 - 1), sh, L));
+  }
+  fetch(coef + (int64_t)(j1 - 1) * ldw, T + R);
+  for (int j = j1; j >= j0; --j) {
+    const int sh = j - 1, st = 1 << sh;
+    const int Win = T + halo(j), Wout = T + halo(j - 1);
+    const int M = ModCm::M(Win, Wout, sh, L);
+    scatter(wb, Win, sh, M);
+    lds_barrier();
+    if (j > j0) fetch(coef + (int64_t)(j - 2) * ldw, Wout);  // next level's W in flight
+    const int nmb = ModCm::nmb(Wout, sh);
+    const int nitems = nmb << sh;
+    double o0[MAXI], o1[MAXI];
+#pragma unroll
+    for (int k = 0; k < MAXI; ++k) {
+      const int u = tid + k * NT;
+      if ((k + 1) * NT <= nitems || u < nitems) {
+        const int base = (u & (st - 1)) * M + 2 * (u >> sh);
+        const double* va = vb + base;
+        const double* wa = wb + base;
+        double xv[L + 2], xw[L + 2];
+#pragma unroll
+        for (int e = 0; e < L + 2; e += 2) {
+          const double2 a = *reinterpret_cast<const double2*>(va + e);
+          const double2 w = *reinterpret_cast<const double2*>(wa + e);
+          xv[e] = a.x;
+          xv[e + 1] = a.y;
+          xw[e] = w.x;
+          xw[e + 1] = w.y;
+        }
+        double sa0 = 0.0, sd0 = 0.0, sa1 = 0.0, sd1 = 0.0;
+#pragma unroll
+        for (int l = 0; l < L; ++l) {
+          sa0 = mac<FMA>(sa0, xv[l], tp.g[l]);
+          sd0 = mac<FMA>(sd0, xw[l], tp.h[l]);
+          sa1 = mac<FMA>(sa1, xv[l + 1], tp.g[l]);
+          sd1 = mac<FMA>(sd1, xw[l + 1], tp.h[l]);
+        }
+        o0[k] = sa0 + sd0;
+        o1[k] = sa1 + sd1;
+      }
+    }
+    lds_barrier();
+    if (j == j0) {
+#pragma unroll
+      for (int k = 0; k < MAXI; ++k) {
+        const int u = tid + k * NT;
+        if ((k + 1) * NT <= nitems || u < nitems) {
+          const int p = (u & (st - 1)) + ((2 * (u >> sh)) << sh);
+          if (p < T && t0 + p < N) dst[t0 + p] = o0[k];
+          if (p + st < T && t0 + p + st < N) dst[t0 + p + st] = o1[k];
+        }
+      }
+    } else {
+      // level j-1 layout: class r' = r mod st/2, m' = 2m + (r >= st/2)
+      const int shn = sh - 1;
+      const int Mn = ModCm::M(Wout, T + halo(j - 2), shn, L);
+#pragma unroll
+      for (int k = 0; k < MAXI; ++k) {
+        const int u = tid + k * NT;
+        if ((k + 1) * NT <= nitems || u < nitems) {
+          const int r = u & (st - 1), m = 2 * (u >> sh);
+          const int p = r + (m << sh);
+          double* ob = vb + (r & ((st >> 1) - 1)) * Mn + 2 * m + (r >> shn);
+          if (p < Wout) ob[0] = o0[k];
+          if (p + st < Wout) ob[2] = o1[k];
+        }
+      }
+      // (the barrier after the next level's W scatter orders these writes)
+    }
+  }
+}
+
 }  // namespace jwv
