@@ -7,8 +7,9 @@
 // Latency rules for the tail, where one wave often works alone:
 //  * every level issues all of its LDS reads before its first FP64 op (one
 //    LDS round trip per level, not one per tap);
-//  * the reverse array-head pairs (Wavelet.java:284-296 order) sum from
-//    registers: no LDS access inside a divergent branch;
+//  * the reverse array-head pairs (Wavelet.java:284-296 order, wave 0 only)
+//    take their runtime-rotated order from LDS (inputs and an LDS copy of the
+//    taps); interior pairs read their inputs without wrapping;
 //  * barriers are LDS-only (lds_barrier), so the detail stores of the forward
 //    levels stay in flight across them.
 // Math and summation order are those of fwt_fwd_res / fwt_rev_res.
@@ -29,23 +30,27 @@ __device__ __forceinline__ void fwd_pair_wrap(const FwdTaps<L>& tp, const double
 }
 
 // Synthesis pair m of a level of size h >= L: a = lds[0, half), d =
-// lds[half, h).  Interior pairs (m >= Q-1) sum q descending; head pairs use
-// rev_pair_head's order on the same register values.
+// lds[half, h).  Interior pairs (m >= Q-1) sum q descending from registers;
+// the array-head pairs (m < Q-1, lanes of wave 0) take rev_pair_head's order
+// through rev_pair_rot_t (inputs and taps tl from LDS, no register select).
 template <int L, bool FMA>
-__device__ __forceinline__ void rev_pair_wrap(const RevTaps<L>& tp, const double* lds, int half,
-                                              int m, double& xe, double& xo) {
+__device__ __forceinline__ void rev_pair_wrap(const RevTaps<L>& tp, const double* tl,
+                                              const double* lds, int half, int m, double& xe,
+                                              double& xo) {
   constexpr int Q = (L + 1) / 2;
   const int hm = half - 1;
-  double av[Q], dv[Q];
+  if (m >= Q - 1) {
+    double av[Q], dv[Q];
 #pragma unroll
-  for (int q = 0; q < Q; ++q) {
-    const int i = (m - q) & hm;
-    av[q] = lds[i];
-    dv[q] = lds[half + i];
+    for (int q = 0; q < Q; ++q) {
+      av[q] = lds[m - q];
+      dv[q] = lds[half + m - q];
+    }
+    rev_pair<L, FMA>(tp, av, dv, -1, xe, xo);  // A[-q * -1] = av[q] = a[m - q]
+  } else {
+    rev_pair_rot_t<L, FMA>(tl, [=](int q) { return lds[(m - q) & hm]; },
+                           [=](int q) { return lds[half + ((m - q) & hm)]; }, m, xe, xo);
   }
-  // interior and head pairs (m < Q-1) on one path: wave 0 holds both kinds
-  rev_pair_rot<L, FMA>(tp, [&](int q) { return av[q]; }, [&](int q) { return dv[q]; },
-                       m < Q - 1 ? m : Q - 1, xe, xo);
   pin2(xe, xo);
 }
 
@@ -151,6 +156,9 @@ __device__ __forceinline__ void rev_res1_levels(double* lds, int h0, int nlev,
                                                 const RevTaps<L>& tp) {
   constexpr int RM = CAP / 2 / NT > 0 ? CAP / 2 / NT : 1;
   const int tid = threadIdx.x;
+  __shared__ __attribute__((aligned(16))) double tl[2 * L];
+  stage_rev_taps<L>(tp, tl);
+  lds_barrier();
   int h = h0, lev = 0;
   if (nlev > 0 && (h >> 1) <= 64) {  // small levels: wave 0 alone
     if (tid < 64) {
@@ -171,7 +179,7 @@ __device__ __forceinline__ void rev_res1_levels(double* lds, int h0, int nlev,
           }
           rev_small_c<L, FMA>(tp, av, dv, 1, hh, m, xe, xo);  // h < L: compile-time h
         } else {
-          rev_pair_wrap<L, FMA>(tp, lds, half, m, xe, xo);
+          rev_pair_wrap<L, FMA>(tp, tl, lds, half, m, xe, xo);
         }
         wave_lds_sync();
         if (v) *reinterpret_cast<double2*>(lds + 2 * m) = make_double2(xe, xo);
@@ -187,7 +195,9 @@ __device__ __forceinline__ void rev_res1_levels(double* lds, int h0, int nlev,
     JWV_STAMP(2 + lev);
     const int half = h >> 1;
     double xe[RM], xo[RM];
-    auto slot = [&](int r) { rev_pair_wrap<L, FMA>(tp, lds, half, tid + r * NT, xe[r], xo[r]); };
+    auto slot = [&](int r) {
+      rev_pair_wrap<L, FMA>(tp, tl, lds, half, tid + r * NT, xe[r], xo[r]);
+    };
     const int R = half / NT;
     if (R <= 1) {
       if (tid < half) slot(0);

@@ -208,6 +208,43 @@ __device__ __forceinline__ void rev_pair_rot(const RevTaps<L>& tp, GA A, GD D, i
   xo = so;
 }
 
+// The same rotated order with the per-term values computed in that order:
+// q = (r - k) mod Q is a runtime index, so the inputs come from LDS (A, D)
+// and the taps from an LDS copy tl (stage_rev_taps) instead of a Q x Q
+// register select.  Bit-identical to rev_pair_rot.  For the array-head lanes
+// only: interior pairs keep rev_pair.
+template <int L, bool FMA, typename GA, typename GD>
+__device__ __forceinline__ void rev_pair_rot_t(const double* tl, GA A, GD D, int r, double& xe,
+                                               double& xo) {
+  static_assert(L >= 2 && (L & 1) == 0, "compiled-in even banks only");
+  constexpr int Q = L / 2;
+  double se = 0.0, so = 0.0;
+#pragma unroll
+  for (int k = 0; k < Q; ++k) {
+    const int q = (r - k) & (Q - 1);
+    const double a = A(q), d = D(q);
+    const double2 lo = *reinterpret_cast<const double2*>(tl + 4 * q);
+    const double2 hi = *reinterpret_cast<const double2*>(tl + 4 * q + 2);
+    se += mac<FMA>(a * lo.x, d, hi.x);
+    so += mac<FMA>(a * lo.y, d, hi.y);
+  }
+  xe = se;
+  xo = so;
+}
+// tl[4q .. 4q+3] = lo_r[2q], lo_r[2q+1], hi_r[2q], hi_r[2q+1] (2L doubles);
+// thread 0 writes, the caller's next block barrier publishes.
+template <int L>
+__device__ __forceinline__ void stage_rev_taps(const RevTaps<L>& tp, double* tl) {
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int q = 0; q < L / 2; ++q) {
+      *reinterpret_cast<double2*>(tl + 4 * q) = make_double2(tp.lo_r[2 * q], tp.lo_r[2 * q + 1]);
+      *reinterpret_cast<double2*>(tl + 4 * q + 2) =
+          make_double2(tp.hi_r[2 * q], tp.hi_r[2 * q + 1]);
+    }
+  }
+}
+
 // Levels with h < L wrap several times: emulate the scatter literally
 // (i ascending, j ascending).  Only for tiny h (h < L <= 64), per output k.
 template <int L, bool FMA>
@@ -555,6 +592,8 @@ __device__ __forceinline__ void fwt_rev_res_blk(const double* __restrict__ s, Ax
   const int tid = threadIdx.x;
   const int htop = nlev > 0 ? (h0 << (nlev - 1)) : h0;
 
+  __shared__ __attribute__((aligned(16))) double tl[2 * (L > 0 ? L : 2)];
+  if constexpr (FB<L>::kStatic) stage_rev_taps<L>(tp, tl);
   JWV_STAMP(0);
   load_window<C, NT, MAXU>(lds, s, htop, dma != 0, c0, inner,
                            [&](int e) { return (int64_t)e * sv.s_len; });
@@ -574,8 +613,8 @@ __device__ __forceinline__ void fwt_rev_res_blk(const double* __restrict__ s, Ax
       if (m >= Q - 1) {
         rev_pair<L, FMA>(tp, lb + m * C, lb + (half + m) * C, C, xe, xo);
       } else {
-        rev_pair_rot<L, FMA>(tp, [=](int q) { return lb[((m - q) & hm) * C]; },
-                             [=](int q) { return lb[(half + ((m - q) & hm)) * C]; }, m, xe, xo);
+        rev_pair_rot_t<L, FMA>(tl, [=](int q) { return lb[((m - q) & hm) * C]; },
+                               [=](int q) { return lb[(half + ((m - q) & hm)) * C]; }, m, xe, xo);
       }
     } else {
       rev_pair_any<L, FMA>(
