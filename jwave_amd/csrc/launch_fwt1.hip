@@ -3,6 +3,7 @@
 // launch_fwt_wpt.hip).  Used for contiguous, 16-B aligned signals with a
 // compiled-in tap count; every other case keeps the generic tile kernels.
 #include "fwt1_kernels.hpp"
+#include <cstdlib>
 #include "fwt1_res.hpp"
 #include "fwt8_kernels.hpp"
 #include "wpt1_kernels.hpp"
@@ -97,30 +98,33 @@ hipError_t rev1_l(const Bank& b, const TileArgs& a, hipStream_t s) {
   }
 }
 
-// resident kernels for a handful of rows (latency-bound tail): 1024 threads
+// resident kernels for a handful of rows (latency-bound tail): 1024 threads;
+// many short rows (the tail under the C = 1 row tile passes): 256 threads,
+// slot loops sized for kRowCap
 constexpr int kCap = Geo::kResCap1;
-template <int L>
+constexpr int kRowCap = 1024;
+template <int L, int NTX, int CAPX>
 hipError_t fwd_res1_l(const Bank& b, const ResArgs& a, hipStream_t s) {
   FwdTaps<L> tp;
   for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
   const size_t lds = (size_t)(a.n + 2) * sizeof(double);
   const dim3 grid((unsigned)a.nouter);
-  auto k = fwt_fwd_res1<L, 1024, kCap, kFMA>;
+  auto k = fwt_fwd_res1<L, NTX, CAPX, kFMA>;
   if (hipError_t e = prep1(k, lds)) return e;
-  hipLaunchKernelGGL(k, grid, dim3(1024), lds, s, a.src, a.sv.s_outer, a.dst, a.dv.s_outer, a.n,
+  hipLaunchKernelGGL(k, grid, dim3(NTX), lds, s, a.src, a.sv.s_outer, a.dst, a.dv.s_outer, a.n,
                      a.nlev, tp);
   return hipGetLastError();
 }
-template <int L>
+template <int L, int NTX, int CAPX>
 hipError_t rev_res1_l(const Bank& b, const ResArgs& a, hipStream_t s) {
   RevTaps<L> tp;
   for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
   const int htop = a.nlev > 0 ? (a.n << (a.nlev - 1)) : a.n;
   const size_t lds = (size_t)(htop + 2) * sizeof(double);
   const dim3 grid((unsigned)a.nouter);
-  auto k = fwt_rev_res1<L, 1024, kCap, kFMA>;
+  auto k = fwt_rev_res1<L, NTX, CAPX, kFMA>;
   if (hipError_t e = prep1(k, lds)) return e;
-  hipLaunchKernelGGL(k, grid, dim3(1024), lds, s, a.src, a.sv.s_outer, a.dst, a.dv.s_outer, a.n,
+  hipLaunchKernelGGL(k, grid, dim3(NTX), lds, s, a.src, a.sv.s_outer, a.dst, a.dv.s_outer, a.n,
                      a.nlev, tp);
   return hipGetLastError();
 }
@@ -224,31 +228,52 @@ bool fwt_fwd_tile1(const Bank& b, const TileArgs& a, hipStream_t s, hipError_t& 
     default: return false;
   }
 }
-// Only for a handful of signals (the latency-bound tail of long 1-D signals):
-// batches of rows keep the generic resident kernels (higher occupancy).
+// A handful of signals (the latency-bound tail of long 1-D signals): 1024
+// threads; batches of rows up to kRowCap: 256 threads (res1_rows).
+// Batches of short rows (<= kRowCap) also take the compiled-in kernels with
+// 256 threads (env JWV_RES1ROWS=0: the generic ones).  Config 3 row tails:
+// fwd 51 -> 41 us, rev ~100 -> 90 us.
+bool res1_rows() {
+  static const bool v = [] {
+    const char* e = std::getenv("JWV_RES1ROWS");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+template <int L>
+hipError_t fwd_res1_pick(const Bank& b, const ResArgs& a, hipStream_t s) {
+  if (a.nouter >= 64) return fwd_res1_l<L, 256, kRowCap>(b, a, s);
+  return fwd_res1_l<L, 1024, kCap>(b, a, s);
+}
+template <int L>
+hipError_t rev_res1_pick(const Bank& b, const ResArgs& a, hipStream_t s) {
+  if (a.nouter >= 64) return rev_res1_l<L, 256, kRowCap>(b, a, s);
+  return rev_res1_l<L, 1024, kCap>(b, a, s);
+}
 bool fwt_fwd_res1(const Bank& b, const ResArgs& a, hipStream_t s, hipError_t& err) {
   if (!Geo::fwt1() || !a.dma || a.inner != 1 || !plain(a.sv) || !plain(a.dv)) return false;
-  if (a.nouter >= 64) return false;
+  if (a.nouter >= 64 && !(res1_rows() && a.n <= kRowCap)) return false;
   if (a.n > kCap || a.n < 2) return false;
   switch (b.L) {
-    case 2: err = fwd_res1_l<2>(b, a, s); return true;
-    case 4: err = fwd_res1_l<4>(b, a, s); return true;
-    case 8: err = fwd_res1_l<8>(b, a, s); return true;
-    case 16: err = fwd_res1_l<16>(b, a, s); return true;
+    case 2: err = fwd_res1_pick<2>(b, a, s); return true;
+    case 4: err = fwd_res1_pick<4>(b, a, s); return true;
+    case 8: err = fwd_res1_pick<8>(b, a, s); return true;
+    case 16: err = fwd_res1_pick<16>(b, a, s); return true;
     default: return false;
   }
 }
 bool fwt_rev_res1(const Bank& b, const ResArgs& a, hipStream_t s, hipError_t& err) {
   if (!Geo::fwt1() || !a.dma || a.inner != 1 || b.scale != 1.0) return false;
-  if (!plain(a.sv) || !plain(a.dv) || a.nouter >= 64) return false;
+  if (!plain(a.sv) || !plain(a.dv)) return false;
   if (((uintptr_t)a.dst & 15) || !even_rows(a.dv, a.nouter)) return false;
   const int64_t htop = a.nlev > 0 ? ((int64_t)a.n << (a.nlev - 1)) : a.n;
+  if (a.nouter >= 64 && !(res1_rows() && htop <= kRowCap)) return false;
   if (htop > kCap || htop < 2) return false;
   switch (b.L) {
-    case 2: err = rev_res1_l<2>(b, a, s); return true;
-    case 4: err = rev_res1_l<4>(b, a, s); return true;
-    case 8: err = rev_res1_l<8>(b, a, s); return true;
-    case 16: err = rev_res1_l<16>(b, a, s); return true;
+    case 2: err = rev_res1_pick<2>(b, a, s); return true;
+    case 4: err = rev_res1_pick<4>(b, a, s); return true;
+    case 8: err = rev_res1_pick<8>(b, a, s); return true;
+    case 16: err = rev_res1_pick<16>(b, a, s); return true;
     default: return false;
   }
 }
