@@ -153,8 +153,41 @@ hipError_t wrev1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a.src, a.sv, a.dst, a.dv, a.h, tp);
   return hipGetLastError();
 }
+// 8192-sample forward WPT tiles, 512 threads: half the halo recompute of the
+// 4096 tile (14.7% -> 7.4% extra pairs) at the same waves per CU.  Config 4
+// forward 2597 -> 2468 us; the reverse (halo ~7% at 4096) measured no gain
+// and keeps 4096.  env JWV_WPT8K=0: 4096 for both.
+template <int L, bool FWD>
+hipError_t wpt8k(const Bank& b, const TileArgs& a, hipStream_t s) {
+  constexpr int TT = 8192, K = 6;
+  const dim3 grid((unsigned)(a.nouter * (a.h / TT)));
+  if constexpr (FWD) {
+    auto k = wpt_fwd_tile1<L, 512, TT, K, kFMA>;
+    const size_t lds = (size_t)Wpt1FwdGeo<L, TT, K>::lds_doubles() * sizeof(double);
+    if (hipError_t e = prep1(k, lds)) return e;
+    FwdTaps<L> tp;
+    for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
+    hipLaunchKernelGGL(k, grid, dim3(512), lds, s, a.src, a.sv, a.dst, a.dv, a.h, tp);
+  } else {
+    auto k = wpt_rev_tile1<L, 512, TT, K, kFMA>;
+    const size_t lds = (size_t)Wpt1RevGeo<L, TT, K>::lds_doubles() * sizeof(double);
+    if (hipError_t e = prep1(k, lds)) return e;
+    RevTaps<L> tp;
+    for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
+    hipLaunchKernelGGL(k, grid, dim3(512), lds, s, a.src, a.sv, a.dst, a.dv, a.h, tp);
+  }
+  return hipGetLastError();
+}
+bool wpt_8k() {
+  static const bool v = [] {
+    const char* e = std::getenv("JWV_WPT8K");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
 template <int L>
 hipError_t wpt1_l(const Bank& b, const TileArgs& a, hipStream_t s, bool fwd) {
+  if (fwd && a.K == 6 && a.h % 8192 == 0 && wpt_8k()) return wpt8k<L, true>(b, a, s);
   switch (a.K) {
     case 1: return fwd ? wfwd1_k<L, 1>(b, a, s) : wrev1_k<L, 1>(b, a, s);
     case 2: return fwd ? wfwd1_k<L, 2>(b, a, s) : wrev1_k<L, 2>(b, a, s);
