@@ -11,7 +11,7 @@ if [ -z "$2" ]; then
 fi
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench_fwt1d.json 2> $O/bench_fwt1d.err || { echo BENCH fwt1d FAILED; tail $O/bench_fwt1d.err; exit 2; }
 for WL in fwt2d wpt modwt; do
-  timeout -k 10 300 python bench.py --workload $WL --steps 10 --warmup 3 > $O/bench_$WL.json 2> $O/bench_$WL.err || { echo BENCH $WL FAILED; tail $O/bench_$WL.err; exit 3; }
+  timeout -k 10 300 python bench.py --workload $WL --steps 30 --warmup 10 > $O/bench_$WL.json 2> $O/bench_$WL.err || { echo BENCH $WL FAILED; tail $O/bench_$WL.err; exit 3; }
 done
 python tools/show_bench.py $O
 bash tools/gpu_pmc.sh $TAG/pmc exact fwt1d fwt2d wpt modwt || exit 4
