@@ -363,7 +363,8 @@ void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
     double* ad = last ? a.dst : c->ws[pp].p;
     const AxisView av = last ? a.dv : cview(h >> K, a.inner);
     jwv::TileArgs t{cur, cv, nullptr, {}, a.dst, a.dv, ad, av, h, K, a.outer, a.inner,
-                    dma_view(cur, cv, C, a.inner), h == a.len ? Geo::store_pol() : 0,
+                    dma_view(cur, cv, C, a.inner),
+                    h == a.len ? Geo::store_pol() | (a.outer == 1 ? Geo::tile_desc(0) : 0) : 0,
                     first1 && h == a.len && Geo::fwd1_first_t() != Geo::kFwt1T
                         ? Geo::fwd1_first_t() : 0};
     { ProfScope ps_(c, h == a.len ? K_FWT_FWD_TILE : K_FWT_FWD_TILE_DEEP,
@@ -458,7 +459,7 @@ void fwt_rev_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
     const AxisView ov = last ? a.dv : cview(hK, a.inner);
     jwv::TileArgs t{acur, acv, a.src, a.sv, out, ov, nullptr, {}, h1, K, a.outer, a.inner,
                     dma_view(acur, acv, C, a.inner) && dma_view(a.src, a.sv, C, a.inner),
-                    last ? Geo::store_pol() : 0};
+                    last ? Geo::store_pol() | (a.outer == 1 ? Geo::tile_desc(1) : 0) : 0};
     { ProfScope ps_(c, last ? K_FWT_REV_TILE : K_FWT_REV_TILE_DEEP, 16.0 * a.outer * hK * a.inner);
     hipchk(jwv::launch_fwt_rev_tile(b, use_fma(c), C, t, c->stream), "fwt_rev_tile"); }
     acur = out;
@@ -943,6 +944,12 @@ int Geo::store_pol() {
   static const int p = env_int("JWV_STPOL", 0);
   return p < 0 || p > 2 ? 0 : p;
 }
+// sp bit 2 for the big pass of one long signal: env JWV_TILE_DESC bit 0 =
+// forward, bit 1 = reverse walks its XCD chunks last-to-first.
+int Geo::tile_desc(int rev) {
+  static const int d = env_int("JWV_TILE_DESC", 0);
+  return ((d >> rev) & 1) << 2;
+}
 int Geo::fwd1_first_t() {
   static const int t = env_int("JWV_FWD1T", kFwt1T) == 1024 ? 1024 : kFwt1T;
   return t;
@@ -1382,7 +1389,7 @@ void body_compress(jwv_ctx* c, const double* x, double* y, int64_t n, double thr
                    double* mag) {
   if (n == 0) return;
   const int np = jwv::compress_partials(n);
-  double* scratch = grow(c, c->red, (size_t)np + 2);
+  double* scratch = grow(c, c->red, (size_t)jwv::compress_scratch(n));
   hipchk(jwv::launch_compress_magnitude(x, y, n, compressor_threshold(threshold), scratch,
                                         c->stream),
          "compress_magnitude");

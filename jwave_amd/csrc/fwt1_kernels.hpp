@@ -113,9 +113,7 @@ __global__ __launch_bounds__(NT) void fwt_fwd_tile1(const double* __restrict__ s
   using G = Fwd1Geo<L, T, K>;
   constexpr int M0 = G::m(0);
   const int ntile = h / T;
-  const int nblk = gridDim.x;
-  int b = blockIdx.x;
-  if ((nblk & 7) == 0) b = (b & 7) * (nblk >> 3) + (b >> 3);
+  const int b = tile_order(gridDim.x, sp);
   const int t = b % ntile;
   const int64_t o = b / ntile;
   const double* s = src + o * s_src;
@@ -291,9 +289,7 @@ __global__ __launch_bounds__(NT) void fwt_rev_tile1(const double* __restrict__ a
   using G = Rev1Geo<L, T, K>;
   constexpr int MAXU = (G::len(1) + NT - 1) / NT;
   const int ntile = hK / T;
-  const int nblk = gridDim.x;
-  int b = blockIdx.x;
-  if ((nblk & 7) == 0) b = (b & 7) * (nblk >> 3) + (b >> 3);
+  const int b = tile_order(gridDim.x, sp);
   const int t = b % ntile;
   const int64_t o = b / ntile;
   const double* sa = asrc + o * s_a;

@@ -250,7 +250,24 @@ __device__ __forceinline__ void st2(double* p, double a, double b) {
 // MI355X_MICROARCH.md "boundary"); 2 nt.  base must be wave-uniform (it
 // becomes the buffer descriptor); off in doubles, < 2^28.
 typedef unsigned int jwv_u32x4 __attribute__((ext_vector_type(4)));
+// Tile of this block in an XCD-chunked walk: consecutive blockIdx go to
+// different XCDs, so XCD x takes the contiguous chunk x of the nblk tiles
+// (its L2 keeps the halo rows); sp bit 2 walks every chunk last-to-first
+// (the next pass then starts on the most recently written, MALL-resident
+// end).  Clears the bit (st2_pol reads sp & 3).
+__device__ __forceinline__ int tile_order(int nblk, int& sp) {
+  const bool desc = (sp & 4) != 0;
+  sp &= 3;
+  const int b = blockIdx.x;
+  if ((nblk & 7) == 0) {
+    const int per = nblk >> 3, j = b >> 3;
+    return (b & 7) * per + (desc ? per - 1 - j : j);
+  }
+  return desc ? nblk - 1 - b : b;
+}
+
 __device__ __forceinline__ void st2_pol(double* base, int off, double a, double b, int sp) {
+  sp &= 3;
   if (sp == 0) {
     *reinterpret_cast<double2*>(base + off) = make_double2(a, b);
     return;

@@ -104,6 +104,7 @@ struct Geo {
   // the first tile pass's details; reverse: the last tile pass): env
   // JWV_STPOL (0 plain, 1 sc1, 2 nt)
   static int store_pol();
+  static int tile_desc(int rev);  // sp bit 2 for the big pass (env JWV_TILE_DESC)
   // First (full-length) forward pass of one long contiguous signal: tile
   // (2048 | 1024, env JWV_FWD1T) and fused levels (env JWV_FWD1K); the last
   // forward tile pass runs down to fwd1_tail() samples (env JWV_FWD1TAIL).
@@ -171,9 +172,11 @@ hipError_t launch_copy_axis(const double* src, AxisView sv, double* dst, AxisVie
                             int64_t nouter, int len, int inner, hipStream_t);
 
 // CompressorMagnitude (launch_compress.hip): y = c with |c| < mean|c| *
-// threshold zeroed; scratch holds compress_partials(n) + 2 doubles (the
-// magnitude lands in scratch[compress_partials(n) + 1]).
+// threshold zeroed, decisions identical to Java's left-to-right magnitude;
+// scratch holds compress_scratch(n) doubles (the magnitude lands in
+// scratch[compress_partials(n) + 1]).
 int compress_partials(int64_t n);
+int compress_scratch(int64_t n);
 hipError_t launch_compress_magnitude(const double* c, double* y, int64_t n, double threshold,
                                      double* scratch, hipStream_t s);
 

@@ -322,8 +322,10 @@ def decompose(x, wavelet, kind="fwt", ctx=None):
 
 def compress_magnitude(x, threshold=1.0, ctx=None):
     """CompressorMagnitude(threshold).compress(x) on the GPU -> (y, magnitude)
-    (compressions/CompressorMagnitude.java:73-84; DESIGN.md: the magnitude sum
-    order differs from the JVM's, so it may differ in the last bits)."""
+    (compressions/CompressorMagnitude.java:73-84).  The kept/zeroed decisions
+    equal Java's for every input; the magnitude is a tree sum (last bits may
+    differ from Java's) unless a coefficient lies within its n*eps band of the
+    cut, in which case it is Java's left-to-right sum (launch_compress.hip)."""
     ctx = _ctx_for(ctx, x)
     n = int(x.shape[0])
     mag = ctypes.c_double(0.0)

@@ -724,6 +724,48 @@ def test_compress_magnitude(ctx, n, thr):
         100.0 * np.count_nonzero(ref == 0) / n if np.count_nonzero(ref == 0) else 0.0)
 
 
+def _thr_at(c, k):
+    """A threshold for which Java's cut (magnitude * threshold, magnitude summed
+    left to right, CompressorMagnitude.java:78-82) equals |c[k]| exactly."""
+    _, mag = oracle.compress_magnitude(c, 1.0)
+    a = abs(float(c[k]))
+    thr = a / mag
+    for _ in range(256):
+        cut = mag * thr
+        if cut == a:
+            return thr
+        thr = float(np.nextafter(thr, np.inf if cut < a else -np.inf))
+    pytest.skip("no threshold hits |c[k]| exactly")
+
+
+@pytest.mark.parametrize("n", [4096, 1 << 20, 1000003])
+def test_compress_magnitude_at_cut(ctx, n):
+    """A coefficient exactly on Java's cut: the tree sum alone cannot decide it
+    (it lies within the n*eps band), so the device forms the left-to-right sum
+    and must keep exactly what Java keeps, with Java's magnitude."""
+    x = rnd(n, seed=11) - 0.5
+    k = n // 3
+    thr = _thr_at(x, k)
+    ref, mag_ref = oracle.compress_magnitude(x, thr)
+    assert ref[k] == x[k]
+    y, mag = jw.compress_magnitude(x, thr, ctx)
+    assert_exact(y, ref, "compress at cut")
+    assert mag == mag_ref  # the serial pass ran: Java's magnitude bit for bit
+
+
+@pytest.mark.parametrize("wname,n,lev", [("Daubechies4", 1 << 16, 16), ("Haar1", 1 << 12, 12)])
+def test_fwt_denoise_at_cut(ctx, wname, n, lev):
+    """In-place compress inside the fused denoise with a coefficient exactly on
+    Java's cut (classify pass, serial magnitude, apply)."""
+    w = jw.by_class(wname)
+    x = rnd(n, seed=13)
+    c = oracle.fwt_forward(w, x, lev)
+    thr = _thr_at(c, n // 2 + 7)
+    cc, _ = oracle.compress_magnitude(c, thr)
+    ref = oracle.fwt_reverse(w, cc, lev)
+    assert_exact(jw.fwt_denoise(x, w, lev, thr, ctx), ref, "denoise at cut")
+
+
 @pytest.mark.parametrize("wname,n,lev", [("Daubechies4", 1 << 16, 16), ("Symlet8", 1 << 20, 12),
                                          ("Haar1", 1 << 10, 10)])
 def test_fwt_denoise(ctx, wname, n, lev):
