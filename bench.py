@@ -527,6 +527,9 @@ def main():
            "dtype": "f64", "data": "synthetic (uniform [0,1) doubles, seed 42+rank)",
            "config": W["config"], "hbm_gbps": round(gbps, 1), "roofline": out_roof,
            "kernels_profiled_pass": kernels, "roundtrip_max_abs_err": err}
+    if not args.dry_run:
+        from jwave_amd import _lib
+        out["build"] = _lib.provenance()  # the library measured: its sources and digest
     if tb is not None:
         out["ms_per_step_with_events"] = round(tb / args.steps * 1e3, 4)
     if out_fp64:

@@ -127,6 +127,16 @@ def header_symbols():
     return sorted(set(re.findall(r"\b(jwv_[a-z0-9_]+)\s*\(", txt)))
 
 
+def provenance():
+    """The in-tree library's build record (lib/libjwave_hip.so.json) and
+    whether it matches the sources of this tree."""
+    from . import _build
+    s = _build.stamp() or {}
+    return {"sources_sha256": s.get("sources_sha256", "")[:16],
+            "lib_sha256": s.get("lib_sha256", "")[:16], "hipcc": s.get("hipcc"),
+            "built_utc": s.get("built_utc"), "matches_sources": not _build.stale()}
+
+
 def lib(path=None):
     """Load libjwave_hip.so (building it first if the sources are newer)."""
     global _lib
@@ -153,6 +163,12 @@ def lib(path=None):
                     raise JWaveError("libjwave_hip.so missing and build failed: %s" % e)
         if not os.path.exists(p):
             raise JWaveError("libjwave_hip.so not found at %s (run __graft_entry__.build())" % p)
+        if not path and not os.environ.get("JWAVE_AMD_LIB"):
+            from . import _build
+            if _build.stale():
+                raise JWaveError("libjwave_hip.so at %s was not built from these sources "
+                                 "(provenance %s); run __graft_entry__.build()"
+                                 % (p, _build.STAMP))
         try:
             L = ctypes.CDLL(p)
         except OSError as e:
