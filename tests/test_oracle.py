@@ -338,3 +338,56 @@ def test_decompose_number_ancient_egyptian():
         jw.decompose_number(100, 24)
     with pytest.raises(jw.JWaveFailure, match="greater than the given number"):
         jw.decompose_number(10, 16)
+
+
+def _tree_sum(a, np_, rb=256):
+    """launch_compress.hip's fixed two-level tree, restated: grid-stride
+    per-thread sums, a block halving tree, then the same over the partials."""
+    def block(vals):
+        red = list(vals) + [0.0] * (rb - len(vals))
+        s = rb // 2
+        while s:
+            for i in range(s):
+                red[i] = red[i] + red[i + s]
+            s //= 2
+        return red[0]
+    n = len(a)
+    partial = []
+    for b in range(np_):
+        th = []
+        for t in range(rb):
+            s = 0.0
+            for i in range(b * rb + t, n, np_ * rb):
+                s += float(a[i])
+            th.append(s)
+        partial.append(block(th))
+    th = []
+    for t in range(rb):
+        s = 0.0
+        for i in range(t, np_, rb):
+            s += partial[i]
+        th.append(s)
+    return block(th)
+
+
+@pytest.mark.parametrize("n,seed,scale", [(1000, 1, 1.0), (4099, 2, 1e-300), (6000, 3, 1e300),
+                                          (2048, 4, 1.0)])
+def test_compress_band_contains_java_cut(n, seed, scale):
+    """The n*eps band of launch_compress.hip around the tree sum always holds
+    Java's left-to-right cut (CompressorMagnitude.java:78-82), so a coefficient
+    outside [cut_lo, cut_hi) is decided as Java decides it."""
+    rng = np.random.default_rng(seed)
+    a = np.abs(rng.standard_normal(n) * rng.choice([1.0, 1e8, 1e-8], n)) * scale
+    np_ = max(1, min(1024, (n + 2047) // 2048))
+    tot = _tree_sum(a, np_)
+    s_j = 0.0
+    for v in a:
+        s_j += float(v)
+    rel = 2.0 * (n + 64.0) * 2.0 ** -53 * 1.01
+    band = tot * rel + (n + 1.0) * 2.0 ** -1074
+    lo = max(float(np.nextafter(tot - band, 0.0)), 0.0)
+    hi = float(np.nextafter(tot + band, np.inf))
+    for thr in (1.0, 0.37, 2.5):
+        cut = lambda s: (s / float(n)) * thr
+        if np.isfinite(hi):
+            assert cut(lo) <= cut(s_j) <= cut(hi)
