@@ -162,7 +162,7 @@ struct Rev1Geo {
 // for alignment) values per operand with 16-B LDS reads at a 16-B lane stride
 // (conflict-free), instead of 2Q 8-B reads per pair.
 #ifndef JWV_REV_COUPLE0
-#define JWV_REV_COUPLE0 0
+#define JWV_REV_COUPLE0 1
 #endif
 template <int L, int NT, int T, int K, bool FMA, int l, bool WT = false, bool CP = false>
 struct Rev1Level {
@@ -180,12 +180,13 @@ struct Rev1Level {
     constexpr int RS = (np + NT - 1) / NT;
     // CP: couples (throughput-bound tile passes; the latency-bound head and
     // chain kernels keep one pair per lane: twice the lanes per level).
-    // Level 0 stores to global memory: one pair per lane keeps those stores
-    // contiguous (a couple's two 16-B stores at a 32-B lane stride cost the
-    // HBM-bound passes more than the LDS reads they save).
     // Short banks (L <= 8: 2Q <= 8 reads per pair) measured slower with
     // couples on the HBM-bound 1D pass (config 2, +1.7 us/step); L = 16 rows
-    // of config 3 gain 11% on the reverse tile.
+    // of config 3 gain 11% on the reverse tile at l > 0, and level 0 (the
+    // global stores, two 16-B stores at a 32-B lane stride) another ~4%
+    // (config 3 rev tiles 362 -> 341 us, 1.418 -> 1.402 ms/step over three
+    // alternating runs on one box; JWV_REV_COUPLE0=0 restores one pair per
+    // lane at level 0).
     constexpr bool kCouple = CP && L >= 12 && (l > 0 || JWV_REV_COUPLE0);
     static_assert(Q - 2 + G::c(l) / 2 < NT, "array-head pairs must sit in slot 0");
     const double* ab = lds + ((((l + 1) & 1) != 0) ? G::buf1() : G::buf0());

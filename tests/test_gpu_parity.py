@@ -753,6 +753,27 @@ def test_compress_magnitude_at_cut(ctx, n):
     assert mag == mag_ref  # the serial pass ran: Java's magnitude bit for bit
 
 
+@pytest.mark.parametrize("special", ["nan", "inf", "overflow", "zeros"])
+def test_compress_magnitude_special_values(ctx, special):
+    """Non-finite and degenerate magnitudes decide as Java's doubles do: a NaN
+    magnitude zeroes everything, an infinite one keeps only infinities, a sum
+    that overflows goes through the left-to-right pass, all-zero input stays
+    zero."""
+    x = rnd(5000, seed=17) - 0.5
+    if special == "nan":
+        x[123] = np.nan
+    elif special == "inf":
+        x[77] = -np.inf
+    elif special == "overflow":
+        x[:] = 1.7e308 * np.sign(x)
+    else:
+        x[:] = 0.0
+    ref, mag_ref = oracle.compress_magnitude(x, 1.0)
+    y, mag = jw.compress_magnitude(x, 1.0, ctx)
+    assert np.array_equal(np.isnan(y), np.isnan(ref))
+    assert_exact(np.nan_to_num(y), np.nan_to_num(ref), "compress " + special)
+
+
 @pytest.mark.parametrize("wname,n,lev", [("Daubechies4", 1 << 16, 16), ("Haar1", 1 << 12, 12)])
 def test_fwt_denoise_at_cut(ctx, wname, n, lev):
     """In-place compress inside the fused denoise with a coefficient exactly on
