@@ -315,6 +315,17 @@ bool try_rev_chain(jwv_ctx* c, const Bank& b, const Axis& a, int h0) {
 // rows, batches) can instead run their top levels through the C = 1 tile
 // kernels and only a short tail resident (config 3 rows: 2.21 -> 1.99 ms per
 // step at 2048).  env JWV_ROWCAP (elements; >= kResCap1 = always resident).
+// Resident reverse cap of row batches on the fwt1 path: the tile pass above
+// it takes the remaining levels (env JWV_REVROWTAIL: 256 | 512 | 1024).
+int rev_row_tail() {
+  static const int t = [] {
+    const char* v = std::getenv("JWV_REVROWTAIL");
+    const int x = v ? std::atoi(v) : Geo::kFwt1RevTail;
+    return (x == 256 || x == 512 || x == 1024) ? x : Geo::kFwt1RevTail;
+  }();
+  return t;
+}
+
 int fwt_res_cap(int C, int64_t outer) {
   static const int rowcap = [] {
     const char* v = std::getenv("JWV_ROWCAP");
@@ -391,7 +402,9 @@ void fwt_rev_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
   // fwt1 path, signal longer than one resident block: the resident tail stops
   // at kFwt1RevTail and the tiled passes take up to kFwt1KMax levels
   const bool f1 = fast1(b, a, true) && a.len > fwt_res_cap(C, a.outer);
-  const int cap = f1 ? Geo::kFwt1RevTail : Geo::res_cap(C);
+  // batches of rows: the resident part stops at rev_row_tail() (env
+  // JWV_REVROWTAIL), one long signal at kFwt1RevTail (the REV_HEAD plan)
+  const int cap = f1 ? (a.outer > 1 ? rev_row_tail() : Geo::kFwt1RevTail) : Geo::res_cap(C);
   const int KM = f1 ? Geo::kFwt1KMax : Geo::fwt_k(C);
   // workspace sizing
   {
