@@ -43,11 +43,13 @@ struct Wpt1FwdLevel {
     constexpr int R = (NC + NT - 1) / NT;
     const int tid = opaque_tid();  // per-level: keeps address math out of the prologue
     double2 ra[R], rd[R];
+    int wo[R];  // write-back offset (2s)*mo + i, kept from the read phase
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int q = tid + r * NT;
       if ((r + 1) * NT <= NC || q < NC) {
         const int s = q / (mo / 2), i = 2 * (q % (mo / 2));  // sub-window, first pair
+        wo[r] = (2 * s) * mo + i;
         const double* in = lds + s * mi + 2 * i;
         double x[L + 2];
 #pragma unroll
@@ -81,9 +83,8 @@ struct Wpt1FwdLevel {
       for (int r = 0; r < R; ++r) {
         const int q = tid + r * NT;
         if ((r + 1) * NT <= NC || q < NC) {
-          const int s = q / (mo / 2), i = 2 * (q % (mo / 2));
-          *reinterpret_cast<double2*>(lds + (2 * s) * mo + i) = ra[r];
-          *reinterpret_cast<double2*>(lds + (2 * s + 1) * mo + i) = rd[r];
+          *reinterpret_cast<double2*>(lds + wo[r]) = ra[r];
+          *reinterpret_cast<double2*>(lds + wo[r] + mo) = rd[r];
         }
       }
       lds_barrier();
@@ -154,6 +155,7 @@ struct Wpt1RevLevel {
     const int pbase = t * (T >> l) - G::c(l - 1) / 2;  // global index of pair 0
     const bool head_tile = pbase < Q - 1;              // block-uniform
     double4 rx[R];
+    int wo[R];  // write-back: (s*lo_ + 2*ml) << 2 | w1 << 1 | w0, kept from the read phase
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int k = tid + r * NT;
@@ -184,7 +186,8 @@ struct Wpt1RevLevel {
           if (w0) *reinterpret_cast<double2*>(yo) = make_double2(x0e, x0o);
           if (w1) *reinterpret_cast<double2*>(yo + 2) = make_double2(x1e, x1o);
         } else {
-          rx[r] = make_double4(x0e, x0o, x1e, x1o);  // store flags recomputed below
+          rx[r] = make_double4(x0e, x0o, x1e, x1o);
+          wo[r] = ((s * lo_ + 2 * ml) << 2) | (w1 ? 2 : 0) | (w0 ? 1 : 0);
         }
       }
     }
@@ -211,14 +214,9 @@ struct Wpt1RevLevel {
       for (int r = 0; r < R; ++r) {
         const int k = tid + r * NT;
         if ((r + 1) * NT <= NC || k < NC) {
-          const int s = k / NCW, ml = 2 * (k % NCW);
-          const int mg = pbase + ml;
-          const bool w0 = !(head_tile && mg >= 0 && mg < Q - 1);
-          const bool w1 = ((NPW % 2 == 0) || ml + 1 < NPW) &&
-                          !(head_tile && mg + 1 >= 0 && mg + 1 < Q - 1);
-          double* ob = lds + s * lo_ + 2 * ml;
-          if (w0) *reinterpret_cast<double2*>(ob) = make_double2(rx[r].x, rx[r].y);
-          if (w1) *reinterpret_cast<double2*>(ob + 2) = make_double2(rx[r].z, rx[r].w);
+          double* ob = lds + (wo[r] >> 2);
+          if (wo[r] & 1) *reinterpret_cast<double2*>(ob) = make_double2(rx[r].x, rx[r].y);
+          if (wo[r] & 2) *reinterpret_cast<double2*>(ob + 2) = make_double2(rx[r].z, rx[r].w);
         }
       }
       if (hs >= 0) *reinterpret_cast<double2*>(lds + hs * lo_ + 2 * hml) = make_double2(hxe, hxo);
