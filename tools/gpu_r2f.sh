@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-2 closing measurement: GPU parity, every workload's bench line (with
-# its CPU baseline and build provenance), rocprofv3 kernel stats for config 2
-# and config 5.  usage: gpu_r2f.sh TAG
+# its CPU baseline and build provenance), rocprofv3 kernel stats for the
+# listed workloads.  usage: gpu_r2f.sh TAG [WORKLOAD...] (default fwt1d modwt)
 set -o pipefail
 export JWAVE_AMD_NO_BUILD=1
 TAG=${1:-r02f}
@@ -15,5 +15,8 @@ for WL in fwt2d wpt modwt; do
   timeout -k 10 300 python bench.py --workload $WL --steps 30 --warmup 10 > $O/bench_$WL.json 2> $O/bench_$WL.err || { echo BENCH $WL FAILED; tail $O/bench_$WL.err; exit 4; }
 done
 python tools/show_bench.py $O
-bash tools/gpu_kstats.sh $TAG/ks_fwt1d fwt1d > $O/ks_fwt1d.txt && cat $O/ks_fwt1d.txt || exit 5
-bash tools/gpu_kstats.sh $TAG/ks_modwt modwt > $O/ks_modwt.txt && cat $O/ks_modwt.txt || exit 6
+shift
+KS="$@"; [ -n "$KS" ] || KS="fwt1d modwt"
+for WL in $KS; do
+  bash tools/gpu_kstats.sh $TAG/ks_$WL $WL > $O/ks_$WL.txt && cat $O/ks_$WL.txt || exit 5
+done
