@@ -173,9 +173,11 @@ int jwv_fwt3d_rev_f64_dev(const double* y, double* x, int64_t p, int64_t q, int6
  * CompressorMagnitude(threshold).compress(double[])
  * (compressions/CompressorMagnitude.java:73-84, Compressor.java:96-110):
  * y[i] = |x[i]| >= m * threshold ? x[i] : 0 with m = sum|x| / n.  A threshold
- * <= 0 becomes 1.0 (Compressor.java:66-80).  m is summed as a fixed tree on
- * the device (deterministic; not the JVM's left-to-right order, so it can
- * differ in the last bits).  magnitude: optional host pointer for m.
+ * <= 0 becomes 1.0 (Compressor.java:66-80).  y equals Java's output for
+ * every input: m is summed as a fixed tree, and only when some |x[i]| lies in
+ * the tree sum's n*eps band around the cut is Java's left-to-right sum formed
+ * on the device and used instead.  magnitude: optional host pointer for m
+ * (the tree value, or Java's when the left-to-right pass ran).
  * jwv_fwt_denoise_*: forward(level) -> compress -> reverse(level) without
  * leaving the device (the Transform + Compressor denoising sequence). */
 int jwv_compress_magnitude_f64(const double* x, double* y, int64_t n, double threshold,
