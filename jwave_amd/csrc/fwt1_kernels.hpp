@@ -35,6 +35,9 @@ struct Fwd1Geo {
   }
 };
 
+#ifndef JWV_FWD_SLOT_FENCE
+#define JWV_FWD_SLOT_FENCE 1
+#endif
 template <int L, int NT, int T, int K, bool FMA, int l, bool WT = false>
 struct Fwd1Level {
   // level l reads the level-(l-1) window at lds + off(l-1) (l = 1: lds) and
@@ -70,6 +73,10 @@ struct Fwd1Level {
         double a0, d0, a1, d1;
         fwd_pair<L, FMA>(tp, [&](int j) { return x[j]; }, a0, d0);
         fwd_pair<L, FMA>(tp, [&](int j) { return x[j + 2]; }, a1, d1);
+        // long banks: a slot boundary keeps the compiler from hoisting every
+        // slot's L+2 window reads at once (L = 16: 118 -> fewer VGPRs)
+        if constexpr (L >= 12 && JWV_FWD_SLOT_FENCE)
+          asm volatile("" : "+v"(a0), "+v"(a1), "+v"(d0), "+v"(d1) :: "memory");
         const int p = 2 * q;
         if constexpr (l == K) {  // WT: handed to another workgroup of this launch
           st2<WT>(ya + (int64_t)t * own + p, a0, a1);
