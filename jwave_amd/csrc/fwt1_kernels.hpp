@@ -38,6 +38,9 @@ struct Fwd1Geo {
 #ifndef JWV_FWD_SLOT_FENCE
 #define JWV_FWD_SLOT_FENCE 1
 #endif
+#ifndef JWV_FWD_FENCE_MINL
+#define JWV_FWD_FENCE_MINL 12
+#endif
 template <int L, int NT, int T, int K, bool FMA, int l, bool WT = false>
 struct Fwd1Level {
   // level l reads the level-(l-1) window at lds + off(l-1) (l = 1: lds) and
@@ -74,8 +77,10 @@ struct Fwd1Level {
         fwd_pair<L, FMA>(tp, [&](int j) { return x[j]; }, a0, d0);
         fwd_pair<L, FMA>(tp, [&](int j) { return x[j + 2]; }, a1, d1);
         // long banks: a slot boundary keeps the compiler from hoisting every
-        // slot's L+2 window reads at once (L = 16: 118 -> fewer VGPRs)
-        if constexpr (L >= 12 && JWV_FWD_SLOT_FENCE)
+        // slot's L+2 window reads at once (L = 16: 118 -> 54 VGPRs, 8 waves
+        // per SIMD).  L = 8 (68 -> 40 VGPRs) measured 1.5% slower on config 2,
+        // so the fence starts at JWV_FWD_FENCE_MINL = 12.
+        if constexpr (L >= JWV_FWD_FENCE_MINL && JWV_FWD_SLOT_FENCE)
           asm volatile("" : "+v"(a0), "+v"(a1), "+v"(d0), "+v"(d1) :: "memory");
         const int p = 2 * q;
         if constexpr (l == K) {  // WT: handed to another workgroup of this launch
