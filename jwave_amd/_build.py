@@ -73,14 +73,17 @@ def _hipcc_version():
 
 def build(force=False, jobs=5):
     compiled = False
-    if force or stale():
+    was_stale = stale()
+    if force or was_stale:
         before = os.path.getmtime(LIB) if os.path.exists(LIB) else None
         jobs = min(int(jobs), 16)
         subprocess.check_call(["make", "-s", "-j%d" % jobs, "-C", CSRC]
                               + (["-B"] if force else []))
         compiled = before is None or os.path.getmtime(LIB) != before
     s = stamp()
-    if compiled or s is None or s.get("lib_sha256") != _file_digest(LIB):
+    # make is the judge of what to recompile (mtimes); the record follows
+    # whenever the sources or the library differ from it
+    if compiled or was_stale or s is None or s.get("lib_sha256") != _file_digest(LIB):
         rec = {"sources_sha256": source_digest(), "lib_sha256": _file_digest(LIB),
                "arch": "gfx950", "hipcc": _hipcc_version(),
                "built_utc": datetime.datetime.utcnow().strftime("%Y-%m-%dT%H:%M:%SZ"),

@@ -67,10 +67,13 @@ hipError_t rev_l(const Bank& b, const ChainRevArgs& a, hipStream_t s) {
                      a.h, a.h0R, a.nR, a.epoch, a.spins, tp);
   return hipGetLastError();
 }
+#ifndef JWV_HEAD_NT
+#define JWV_HEAD_NT 512
+#endif
 template <int L>
 hipError_t head_l(const Bank& b, const RevHeadArgs& a, hipStream_t s) {
   // 512 threads: the wide levels of R and M take half the pair slots
-  constexpr int NTH = 512;
+  constexpr int NTH = JWV_HEAD_NT;
   auto k = fwt_rev_head1<L, NTH, CG::kCap, CG::kTM, CG::kKM, kFMA>;
   const int hR = a.h0R << (a.nR - 1), nM = (hR << CG::kKM) / CG::kTM;
   if (hR > CG::kCap || nM < 1) return hipErrorInvalidValue;
