@@ -177,7 +177,8 @@ int jwv_fwt3d_rev_f64_dev(const double* y, double* x, int64_t p, int64_t q, int6
  * every input: m is summed as a fixed tree, and only when some |x[i]| lies in
  * the tree sum's n*eps band around the cut is Java's left-to-right sum formed
  * on the device and used instead.  magnitude: optional host pointer for m
- * (the tree value, or Java's when the left-to-right pass ran).
+ * (the tree value, or Java's when the left-to-right pass ran).  x == y (in
+ * place) is allowed; partially overlapping x and y are JWV_ERR_BAD_CALL.
  * jwv_fwt_denoise_*: forward(level) -> compress -> reverse(level) without
  * leaving the device (the Transform + Compressor denoising sequence). */
 int jwv_compress_magnitude_f64(const double* x, double* y, int64_t n, double threshold,

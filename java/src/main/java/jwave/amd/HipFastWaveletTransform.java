@@ -58,6 +58,8 @@ public class HipFastWaveletTransform extends FastWaveletTransform {
       return super.decompose( arrTime );
     int n = arrTime.length;
     int rows = 32 - Integer.numberOfLeadingZeros( Math.max( n, 1 ) );  // log2 n + 1 for 2^p
+    if( !HipNative.fitsArray( rows, n ) )  // (log2 n + 1) * n > one Java array
+      return super.decompose( arrTime );
     double[ ] mat = new double[ rows * n ];
     HipNative.Taps t = _taps;
     HipNative.check( HipNative.decompose( HipNative.ctx( ), _kind, arrTime, mat, t.L, t.tw,
@@ -72,14 +74,14 @@ public class HipFastWaveletTransform extends FastWaveletTransform {
 
   @Override public double[ ][ ] forward( double[ ][ ] m, int lvlM, int lvlN )
       throws JWaveException {
-    if( _taps == null )
+    if( _taps == null || !HipNative.fitsArray( m.length, m.length == 0 ? 0 : m[ 0 ].length ) )
       return super.forward( m, lvlM, lvlN );
     return run2d( true, m, lvlM, lvlN );
   }
 
   @Override public double[ ][ ] reverse( double[ ][ ] m, int lvlM, int lvlN )
       throws JWaveException {
-    if( _taps == null )
+    if( _taps == null || !HipNative.fitsArray( m.length, m.length == 0 ? 0 : m[ 0 ].length ) )
       return super.reverse( m, lvlM, lvlN );
     return run2d( false, m, lvlM, lvlN );
   }
@@ -96,16 +98,21 @@ public class HipFastWaveletTransform extends FastWaveletTransform {
 
   @Override public double[ ][ ][ ] forward( double[ ][ ][ ] s, int lvlP, int lvlQ, int lvlR )
       throws JWaveException {
-    if( _taps == null )
+    if( _taps == null || !fits3d( s ) )
       return super.forward( s, lvlP, lvlQ, lvlR );
     return run3d( true, s, lvlP, lvlQ, lvlR );
   }
 
   @Override public double[ ][ ][ ] reverse( double[ ][ ][ ] s, int lvlP, int lvlQ, int lvlR )
       throws JWaveException {
-    if( _taps == null )
+    if( _taps == null || !fits3d( s ) )
       return super.reverse( s, lvlP, lvlQ, lvlR );
     return run3d( false, s, lvlP, lvlQ, lvlR );
+  }
+
+  private static boolean fits3d( double[ ][ ][ ] s ) {
+    long P = s.length, Q = P == 0 ? 0 : s[ 0 ].length, R = Q == 0 ? 0 : s[ 0 ][ 0 ].length;
+    return HipNative.fitsArray( P * Q, R );
   }
 
   private double[ ][ ][ ] run3d( boolean fwd, double[ ][ ][ ] s, int lp, int lq, int lr )

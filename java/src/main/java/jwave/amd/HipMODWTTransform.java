@@ -22,6 +22,8 @@ public class HipMODWTTransform extends MODWTTransform {
     if( _taps == null || data == null || data.length == 0 )
       return super.forwardMODWT( data, maxLevel ); // reference checks + empty rows
     int n = data.length;
+    if( maxLevel < 0 || !HipNative.fitsArray( maxLevel + 1, n ) )
+      return super.forwardMODWT( data, maxLevel );  // reference checks, or > one Java array
     double[ ] wv = new double[ ( maxLevel + 1 ) * n ];
     try {
       HipNative.check( HipNative.modwt( HipNative.ctx( ), true, data, wv, n, maxLevel, _taps.L,
@@ -36,6 +38,8 @@ public class HipMODWTTransform extends MODWTTransform {
     if( _taps == null || c == null || c.length <= 1 )
       return super.inverseMODWT( c );
     int J = c.length - 1, n = c[ 0 ].length;
+    if( !HipNative.fitsArray( J + 1, n ) )
+      return super.inverseMODWT( c );
     double[ ] wv = HipNative.pack( c ), x = new double[ n ];
     try {
       HipNative.check( HipNative.modwt( HipNative.ctx( ), false, x, wv, n, J, _taps.L, _taps.tw,

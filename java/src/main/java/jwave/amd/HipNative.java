@@ -128,8 +128,17 @@ public final class HipNative {
         t.hiR );
   }
 
+  /** rows * cols doubles fit one Java array (the int product would
+   *  overflow past 2^31 - 1; VMs cap arrays a few elements below that). */
+  static boolean fitsArray( long rows, long cols ) {
+    return rows * cols <= Integer.MAX_VALUE - 8;
+  }
+
   static double[ ] pack( double[ ][ ] m ) {
     int rows = m.length, cols = rows == 0 ? 0 : m[ 0 ].length;
+    if( !fitsArray( rows, cols ) )  // callers check first and keep the Java path
+      throw new IllegalArgumentException( "HipNative#pack - " + rows + " x " + cols
+          + " doubles exceed one Java array" );
     double[ ] out = new double[ rows * cols ];
     for( int i = 0; i < rows; i++ )
       System.arraycopy( m[ i ], 0, out, i * cols, cols );

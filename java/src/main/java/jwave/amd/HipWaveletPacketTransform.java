@@ -40,6 +40,8 @@ public class HipWaveletPacketTransform extends WaveletPacketTransform {
       return super.decompose( arrTime );
     int n = arrTime.length;
     int rows = 32 - Integer.numberOfLeadingZeros( Math.max( n, 1 ) );
+    if( !HipNative.fitsArray( rows, n ) )  // (log2 n + 1) * n > one Java array
+      return super.decompose( arrTime );
     double[ ] mat = new double[ rows * n ];
     HipNative.Taps t = _taps;
     HipNative.check( HipNative.decompose( HipNative.ctx( ), 1, arrTime, mat, t.L, t.tw, t.scale,
@@ -61,7 +63,7 @@ public class HipWaveletPacketTransform extends WaveletPacketTransform {
 
   private double[ ][ ] batch( boolean fwd, double[ ][ ] m, int level ) throws JWaveException {
     int rows = m.length, cols = rows == 0 ? 0 : m[ 0 ].length;
-    if( _taps == null ) {
+    if( _taps == null || !HipNative.fitsArray( rows, cols ) ) {
       double[ ][ ] out = new double[ rows ][ ];
       for( int i = 0; i < rows; i++ )
         out[ i ] = fwd ? super.forward( m[ i ], level ) : super.reverse( m[ i ], level );

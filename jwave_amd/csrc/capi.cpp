@@ -25,6 +25,7 @@
 
 #include "../../include/jwave_hip.h"
 #include "jwv_launch.hpp"
+#include "jwv_stream.hpp"
 
 using jwv::AxisView;
 using jwv::Bank;
@@ -171,8 +172,12 @@ hipEvent_t take_event(jwv_ctx* c) {
     c->ev_pool.pop_back();
     return e;
   }
+  // timing-only events: no system-scope release when the event completes.
+  // The default event writes back and invalidates the caches after the
+  // bracketed kernel (~6 us per 2^24 pass on config 2), which the kernel's
+  // own time does not include (rocprofv3 durations).
   hipEvent_t e;
-  hipchk(hipEventCreate(&e), "hipEventCreate");
+  hipchk(hipEventCreateWithFlags(&e, hipEventDisableSystemFence), "hipEventCreate");
   return e;
 }
 
@@ -335,6 +340,16 @@ int fwt_res_cap(int C, int64_t outer) {
   return Geo::res_cap(C);
 }
 
+// env JWV_FWD1S (default 0): the first forward pass of contiguous signals on
+// the persistent grid of fwt1_stream.hpp instead of one block per tile
+bool fwd_stream1() {
+  static const bool v = [] {
+    const char* e = std::getenv("JWV_FWD1S");
+    return e && std::atoi(e) != 0;
+  }();
+  return v;
+}
+
 void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
   const int nlev = fwd_levels(a.len, b.tw, level);
   if (nlev == 0) return copy_axis(c, a);
@@ -380,7 +395,14 @@ void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
                         ? Geo::fwd1_first_t() : 0};
     { ProfScope ps_(c, h == a.len ? K_FWT_FWD_TILE : K_FWT_FWD_TILE_DEEP,
                     16.0 * a.outer * h * a.inner);
-    hipchk(jwv::launch_fwt_fwd_tile(b, use_fma(c), C, t, c->stream), "fwt_fwd_tile"); }
+      hipError_t e = hipSuccess;
+      // the full-length pass as a persistent double-buffered grid
+      // (fwt1_stream.hpp) where it covers the case
+      const bool st = C == 1 && h == a.len && fwd_stream1() &&
+                      (use_fma(c) ? jwv::fused::fwt_fwd_stream1(b, t, c->stream, e)
+                                  : jwv::exact::fwt_fwd_stream1(b, t, c->stream, e));
+      if (!st) e = jwv::launch_fwt_fwd_tile(b, use_fma(c), C, t, c->stream);
+      hipchk(e, "fwt_fwd_tile"); }
     cur = ad;
     cv = av;
     h >>= K;
@@ -631,13 +653,28 @@ void check_overlap(const double* x, size_t nx, const double* y, size_t ny) {
     throw Fail{JWV_ERR_BAD_CALL, "output buffer overlaps input buffer"};
 }
 
+// The calling thread's current device, restored when the entry returns: a
+// caller (torch, another library) working on another device is not silently
+// re-pointed at the context's.
+struct DeviceScope {
+  int prev = -1;
+  explicit DeviceScope(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) hipchk(hipSetDevice(dev), "hipSetDevice");
+  }
+  ~DeviceScope() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
 template <typename F>
 int guarded(jwv_ctx* c, F&& f) {
   if (!c) return set_err(nullptr, JWV_ERR_BAD_CALL, "jwv_ctx is NULL");
   std::lock_guard<std::mutex> lk(c->mu);
   try {
     c->err.clear();
-    hipchk(hipSetDevice(c->device), "hipSetDevice");
+    DeviceScope ds(c->device);
     f();
     return JWV_OK;
   } catch (const Fail& e) {
@@ -1445,6 +1482,9 @@ int jwv_compress_magnitude_f64_dev(const double* x, double* y, int64_t n, double
     if (n < 0) throw Fail{JWV_ERR_BAD_CALL, "n < 0"};
     if (n == 0) return;
     need_device_ptrs(c, x, y);
+    // exact aliasing takes the in-place (classify-first) path; any partial
+    // overlap would let the first pass's stores reach inputs of later passes
+    if (x != y) check_overlap(x, (size_t)n, y, (size_t)n);
     body_compress(c, x, y, n, threshold, magnitude);
   });
 }

@@ -93,8 +93,10 @@ struct AnyTaps {
 // stores).  The issuing wave must `s_waitcnt vmcnt(0)` itself (asm) before a
 // barrier that publishes the data.  lds_dst must be wave-uniform.
 __device__ __forceinline__ void dma16_asm(const void* g, double* lds_dst) {
-  const unsigned lds_addr =
-      (unsigned)(uintptr_t)((__attribute__((address_space(3))) double*)lds_dst);
+  // wave-uniform by contract; readfirstlane lets the compiler keep it in an
+  // SGPR even when it cannot prove the uniformity itself
+  const unsigned lds_addr = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)((__attribute__((address_space(3))) double*)lds_dst));
   asm volatile(
       "s_mov_b32 m0, %1\n\t"
       "s_nop 0\n\t"

@@ -515,8 +515,19 @@ class WaveletTransform(BasicTransform):
     # WaveletTransform.decompose / recompose (:136-182)
     def decompose(self, arr):
         """All levels at once: row p = forward(arr, p), p = 0..log2 n, one
-        native call (jwv_decompose_f64)."""
-        return decompose(arr, self._wavelet, self.kind, self._ctx)
+        native call (jwv_decompose_f64).  Transforms without a native
+        decompose (MODWT) run the reference loop itself, row p = the first n
+        values of forward(arr, p) (:136-145); for MODWT that raises at p = 0
+        exactly as the reference does (forwardMODWT rejects level 0,
+        MODWTTransform.java:257-260)."""
+        if self.kind in ("fwt", "wpt"):
+            return decompose(arr, self._wavelet, self.kind, self._ctx)
+        a = np.asarray(arr, dtype=np.float64)
+        n = len(a)
+        if not is_binary(n):
+            raise JWaveFailure("BasicTransform#calcExponent - given number is not binary: "
+                               "2^p | pEN .. = 1, 2, 4, 8, 16, 32, .. ")
+        return np.stack([np.asarray(self.forward_1d(a, p))[:n] for p in range(get_exponent(n) + 1)])
 
     def recompose(self, mat, level=None):
         if level is None:

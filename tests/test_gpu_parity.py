@@ -171,9 +171,16 @@ def test_dev_entry_rejects_foreign_pointers(ctx):
         b"not a HIP device pointer" in lib.jwv_last_error(ctx.handle)
 
 
-def test_fwt_config2_full_size(ctx):
+# north_star gate: the forward -> reverse round trip matches the Java
+# reference's round trip within 1e-12 max-abs on the same inputs.  EXACT math
+# is bit-identical (0); FMA math is held to the gate itself.
+RT_GATE = 1e-12
+
+
+def test_fwt_config2_full_size(ctx, ctx_fma):
     """Config 2: Daubechies4, N = 2^24, full depth — exact vs oracle, and the
-    round trip vs the input (reported bound from the taps' precision)."""
+    round trip vs the input (reported bound from the taps' precision).  FMA:
+    round trip within RT_GATE of the oracle's (Java-order) round trip."""
     w = jw.by_class("Daubechies4")
     n = 1 << 24
     x = rnd(n, 42)
@@ -181,8 +188,11 @@ def test_fwt_config2_full_size(ctx):
     yr = oracle.fwt_forward(w, x, 24)
     assert_exact(y, yr, "D4 2^24 fwd")
     xr = T.fwt_reverse(y, w, 24, ctx)
-    assert_exact(xr, oracle.fwt_reverse(w, yr, 24), "D4 2^24 rev")
+    xr_ref = oracle.fwt_reverse(w, yr, 24)
+    assert_exact(xr, xr_ref, "D4 2^24 rev")
     assert np.abs(xr - x).max() < 1e-11
+    rt = T.fwt_reverse(T.fwt_forward(x, w, 24, ctx_fma), w, 24, ctx_fma)
+    assert np.abs(rt - xr_ref).max() <= RT_GATE
 
 
 # ------------------------------------------------------------------ WPT
@@ -223,6 +233,39 @@ def test_wpt_config4_shape(ctx, ctx_fma):
     assert_exact(T.wpt_reverse(yr, w, 6, ctx), xr_ref, "wpt cfg4 rev")
     assert_close(T.wpt_forward(x, w, 6, ctx_fma), yr, "wpt cfg4 fwd fma")
     assert_close(T.wpt_reverse(yr, w, 6, ctx_fma), xr_ref, "wpt cfg4 rev fma")
+
+
+def test_wpt_config4_full_batch(ctx, ctx_fma):
+    """Config 4 at its full shape in ONE call per direction: 4096 Symlet8
+    signals x 65536, 6 levels (WaveletPacketTransform.java:73-191 per signal),
+    2 GiB per buffer.  Sampled signals -- first, last, both sides of the
+    signal-2048 midpoint (byte offset 2^30) and the last signal (ending at
+    byte 2^31) -- are bit-exact against the oracle in EXACT math.  FMA math:
+    the round trip's absolute error against the oracle's EXACT round trip is
+    <= 1e-12 (the north_star gate), on the sampled signals and, against the
+    input, on the whole batch."""
+    import torch
+    B, n, lev = 4096, 1 << 16, 6
+    w = jw.by_class("Symlet8")
+    gen = torch.Generator(device="cuda:0").manual_seed(4096)
+    x = torch.rand(B, n, dtype=torch.float64, device="cuda:0", generator=gen)
+    sample = [0, 1, 777, 2047, 2048, 2049, 3333, 4094, 4095]
+    xs = x[sample].cpu().numpy()
+    y = T.wpt_forward(x, w, lev, ctx)
+    ys_ref = oracle.batch("wpt", True, w, xs, lev)
+    assert_exact(y[sample].cpu().numpy(), ys_ref, "wpt cfg4 full batch fwd")
+    xr = T.wpt_reverse(y, w, lev, ctx)
+    xrs_ref = oracle.batch("wpt", False, w, ys_ref, lev)
+    assert_exact(xr[sample].cpu().numpy(), xrs_ref, "wpt cfg4 full batch rev")
+    del xr, y
+    yf = T.wpt_forward(x, w, lev, ctx_fma)
+    xrf = T.wpt_reverse(yf, w, lev, ctx_fma)
+    del yf
+    rt_vs_exact = float(np.abs(xrf[sample].cpu().numpy() - xrs_ref).max())
+    rt_vs_input = float((xrf - x).abs().max().item())
+    assert rt_vs_exact <= 1e-12, "FMA round trip vs EXACT round trip: %g" % rt_vs_exact
+    assert rt_vs_input <= 1e-12, "FMA round trip vs input: %g" % rt_vs_input
+    torch.cuda.synchronize()
 
 
 # ------------------------------------------------------------------ 2-D / 3-D
@@ -312,6 +355,10 @@ def test_fwt2d_config3_full_size(ctx, ctx_fma):
     assert_exact(got, xr, "config 3 rev")
     assert_close(T.transform_2d(yr, w, 13, 13, False, ctx_fma), xr, "config 3 rev fma")
     assert np.abs(got - x).max() < 1e-10
+    del got
+    rt = T.transform_2d(T.transform_2d(x, w, 13, 13, True, ctx_fma), w, 13, 13, False, ctx_fma)
+    d = float(np.abs(rt - xr).max())
+    assert d <= RT_GATE, "config 3 FMA round trip vs oracle round trip: %g" % d
 
 
 @pytest.mark.parametrize("wname", ["Haar1", "Daubechies4", "Symlet8"])
@@ -325,19 +372,27 @@ def test_wpt2d(ctx, wname):
                  oracle.transform_2d("wpt", False, w, yr, 6, 7), "wpt2d rev")
 
 
+@pytest.mark.parametrize("kind", ["fwt", "wpt"])
 @pytest.mark.parametrize("wname", ["Haar1", "Daubechies4", "Daubechies8"])
 @pytest.mark.parametrize("shape", [(2, 4, 8), (16, 32, 64), (8, 8, 8), (64, 16, 2048)])
-def test_3d(ctx, wname, shape):
+def test_3d(ctx, kind, wname, shape):
+    """3-D BasicTransform.forward/reverse (BasicTransform.java:487-659) for the
+    FWT and for the packet transform (jwv_wpt3d_*, the Java plugin's 3-D WPT
+    route) against the oracle's restatement, every axis at full depth."""
     w = jw.by_class(wname)
     p, q, r = shape
     x = rnd(p * q * r, 17).reshape(shape)
     # levels as the reference applies them: (lvlP on Q, lvlQ on R, lvlR on P)
     lp, lq, lr = q.bit_length() - 1, r.bit_length() - 1, p.bit_length() - 1
-    y = T.transform_3d(x, w, lp, lq, lr, True, ctx)
-    yr = oracle.transform_3d("fwt", True, w, x, lp, lq, lr)
-    assert_exact(y, yr, "3d fwd")
-    assert_exact(T.transform_3d(yr, w, lp, lq, lr, False, ctx),
-                 oracle.transform_3d("fwt", False, w, yr, lp, lq, lr), "3d rev")
+    y = T.transform_3d(x, w, lp, lq, lr, True, ctx, kind=kind)
+    yr = oracle.transform_3d(kind, True, w, x, lp, lq, lr)
+    assert_exact(y, yr, "%s 3d fwd" % kind)
+    assert_exact(T.transform_3d(yr, w, lp, lq, lr, False, ctx, kind=kind),
+                 oracle.transform_3d(kind, False, w, yr, lp, lq, lr), "%s 3d rev" % kind)
+    if kind == "wpt":  # partial depth on every axis as well
+        y = T.transform_3d(x, w, lp // 2, lq // 2, lr // 2, True, ctx, kind=kind)
+        assert_exact(y, oracle.transform_3d(kind, True, w, x, lp // 2, lq // 2, lr // 2),
+                     "wpt 3d fwd partial")
 
 
 # ------------------------------------------------------------------ MODWT
@@ -378,7 +433,10 @@ def test_modwt_config5_full_size(ctx, ctx_fma):
     xr = T.modwt_inverse(c, w, ctx)
     assert_exact(xr, oracle.modwt_inverse(w, cr), "imodwt 1e7")
     assert np.abs(xr - x).max() < 1e-10
-    assert_close(T.modwt_forward(x, w, 8, ctx_fma), cr, "modwt fma")
+    cf = T.modwt_forward(x, w, 8, ctx_fma)
+    assert_close(cf, cr, "modwt fma")
+    d = float(np.abs(T.modwt_inverse(cf, w, ctx_fma) - oracle.modwt_inverse(w, cr)).max())
+    assert d <= RT_GATE, "config 5 FMA round trip vs oracle round trip: %g" % d
 
 
 def test_modwt_direct_vs_sparse_oracle():

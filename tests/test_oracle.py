@@ -154,6 +154,14 @@ def test_modwt_flattened_host_logic(monkeypatch):
         m.forward(np.zeros(1 << 14))  # full depth 14 > 13: forwardMODWT's IllegalArgumentException
     with pytest.raises(ValueError, match="at least 1"):
         m.forward(np.zeros(8), 0)
+    # WaveletTransform.decompose (WaveletTransform.java:136-145) is inherited
+    # by MODWTTransform: its row 0 is forward(arr, 0), which forwardMODWT
+    # rejects (MODWTTransform.java:257-260) -- IllegalArgumentException, not a
+    # lookup error of the native decompose
+    with pytest.raises(ValueError, match="at least 1"):
+        m.decompose(np.zeros(8))
+    with pytest.raises(jw.JWaveFailure, match="calcExponent"):
+        m.decompose(np.zeros(6))
 
 
 @pytest.mark.parametrize("w", CREATE2ARR[:20] + CREATE2ARR[25:32], ids=lambda w: w.name)
