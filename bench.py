@@ -455,6 +455,80 @@ def secondary_wpt(args, d):
     return out
 
 
+def host_entry(args, d, reps=5):
+    """SURVEY 8(d) secondary reporting: the drop-in host path end to end
+    (Transform.forward(double[]) -> FastWaveletTransform, Transform.java:81-90):
+    jwv_fwt_fwd_f64 + jwv_fwt_rev_f64 on host arrays of config 2, pageable
+    (what a JNI caller without staging hands over) and page-locked
+    (jwv_host_alloc: what the JNI shim copies Java arrays into), next to the
+    bare PCIe time of the same bytes (pinned H2D + D2H of the 128 MiB array,
+    per direction)."""
+    import numpy as np
+    import torch
+    import jwave_amd as jw
+    from jwave_amd import _lib as L
+    from jwave_amd.transforms import _TapsHolder
+    lib = L.lib()
+    n = 1 << 24
+    w = jw.by_class("Daubechies4")
+    t = _TapsHolder.of(w)
+    ctx = jw.Context(d.local, args.math)
+    h = ctx.handle
+    dp = ctypes.POINTER(ctypes.c_double)
+    x = np.random.default_rng(7).random(n)
+    y = np.empty(n)
+    xr = np.empty(n)
+
+    def step(a, b, c):
+        for fn, src, dst in ((lib.jwv_fwt_fwd_f64, a, b), (lib.jwv_fwt_rev_f64, b, c)):
+            if fn(src.ctypes.data_as(dp), dst.ctypes.data_as(dp), n, 24, t, h):
+                raise RuntimeError(lib.jwv_last_error(h).decode())
+
+    def per_step(f):
+        f()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            f()
+        return (time.perf_counter() - t0) / reps * 1e3
+
+    out = {"workload": "config 2 (D4, N=2^24, full depth) through the host-pointer entries, "
+                       "forward + reverse per step", "steps": reps}
+    out["pageable_ms_per_step"] = round(per_step(lambda: step(x, y, xr)), 3)
+    err = float(np.abs(xr - x).max())
+    bufs = [ctypes.c_void_p() for _ in range(3)]
+    try:
+        for b in bufs:
+            if lib.jwv_host_alloc(h, n * 8, ctypes.byref(b)):
+                raise RuntimeError(lib.jwv_last_error(h).decode())
+        px, py, pr = [np.ctypeslib.as_array((ctypes.c_double * n).from_address(b.value))
+                      for b in bufs]
+        px[:] = x
+        out["pinned_ms_per_step"] = round(per_step(lambda: step(px, py, pr)), 3)
+        err = max(err, float(np.abs(pr - x).max()))
+        # the bare link: the same bytes H2D then D2H, pinned, per direction
+        dev = torch.empty(n, dtype=torch.float64, device=d.dev)
+        tx = torch.from_numpy(px)
+        ty = torch.from_numpy(py)
+
+        def link():
+            dev.copy_(tx, non_blocking=True)
+            ty.copy_(dev, non_blocking=True)
+            torch.cuda.synchronize(d.dev)
+
+        pcie = per_step(link)
+    finally:
+        for b in bufs:
+            if b.value:
+                lib.jwv_host_free(h, b)
+    ctx.close()
+    out["pcie_h2d_plus_d2h_ms_per_direction"] = round(pcie, 3)
+    out["pinned_over_pcie"] = round(out["pinned_ms_per_step"] / (2 * pcie), 3)
+    out["pageable_over_pcie"] = round(out["pageable_ms_per_step"] / (2 * pcie), 3)
+    out["pinned_GBps"] = round(2 * 16.0 * n / (out["pinned_ms_per_step"] * 1e-3) / 1e9, 1)
+    out["roundtrip_max_abs_err"] = err
+    return out
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -536,7 +610,11 @@ def main():
         out["roofline_fp64"] = out_fp64
     if (not args.dry_run and args.workload == "fwt1d" and not args.no_secondary):
         out["batched_wpt_strong"] = secondary_wpt(args, d)
-    if d.rank == 0 and world == 1 and W["cpu"] and not args.no_cpu_baseline:
+        if d.rank == 0:
+            out["host_entry"] = host_entry(args, d)
+    # the reference's CPU path on this node's host cores, in the same run, at
+    # every world size (rank 0, after every GPU leg)
+    if d.rank == 0 and W["cpu"] and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(W["cpu"], args.cpu_seconds)
     else:
         out["cpu_baseline"] = None

@@ -117,6 +117,16 @@ int jwv_ctx_profile_read(jwv_ctx* ctx, jwv_kernel_stat* out, int max_out, int* n
 int jwv_ctx_profile_select(jwv_ctx* ctx, const char* kind);
 /* Release cached device workspace. */
 int jwv_ctx_trim(jwv_ctx* ctx);
+
+/* Page-locked host memory for the host-pointer entry points.  The host entry
+ * points (no _dev suffix) stage pageable arrays through a pinned ring in
+ * chunks (host copies overlapped with the DMA); arrays that are already
+ * page-locked -- from jwv_host_alloc, hipHostMalloc or hipHostRegister -- are
+ * DMA'd directly.  The JNI shim copies Java arrays into such a buffer with
+ * Get/SetDoubleArrayRegion instead of holding a critical region across the
+ * GPU work.  No Java counterpart (boundary plumbing). */
+int jwv_host_alloc(jwv_ctx* ctx, int64_t bytes, void** p);
+int jwv_host_free(jwv_ctx* ctx, void* p);
 int jwv_version(void);
 
 /* ---- 1-D FWT ---------------------------------------------------------------

@@ -67,6 +67,8 @@ _SIGS = {
     "jwv_ctx_synchronize": [_CTX],
     "jwv_ctx_set_poll_limit": [_CTX, ctypes.c_uint],
     "jwv_ctx_trim": [_CTX],
+    "jwv_host_alloc": [_CTX, _i64, ctypes.POINTER(ctypes.c_void_p)],
+    "jwv_host_free": [_CTX, ctypes.c_void_p],
     "jwv_ctx_profile_enable": [_CTX, _int],
     "jwv_ctx_profile_select": [_CTX, ctypes.c_char_p],
     "jwv_ctx_profile_read": [_CTX, ctypes.POINTER(KernelStat), _int, ctypes.POINTER(_int)],

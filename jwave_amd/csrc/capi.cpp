@@ -19,7 +19,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
+#include <functional>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -40,6 +43,84 @@ struct DevBuf {
   size_t n = 0;  // doubles
 };
 
+// Host staging of the host-pointer entry points (Transform.forward(double[])
+// semantics: host array in, host array out).  Pageable caller memory goes
+// through a ring of pinned chunks: host threads copy chunk k into a pinned
+// slot while the DMA engine moves chunk k-1 to the device (and the reverse
+// on the way out), so the PCIe transfer runs at the pinned rate instead of
+// the driver's pageable path.  Pinned caller memory (hipHostMalloc /
+// jwv_host_alloc / hipHostRegister) is DMA'd directly.
+constexpr size_t kPinChunk = size_t(8) << 20;  // bytes per slot
+constexpr int kPinSlots = 4;
+
+// A few host threads for the pageable <-> pinned copies (one core's memcpy
+// is several times slower than the PCIe link).
+class CopyPool {
+ public:
+  explicit CopyPool(int n) {
+    for (int i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  int size() const { return (int)th_.size() + 1; }
+  // memcpy split over the pool's threads and the caller; returns when done
+  void copy(void* dst, const void* src, size_t bytes) {
+    const int parts = bytes >= (size_t(1) << 20) ? size() : 1;
+    if (parts == 1) {
+      std::memcpy(dst, src, bytes);
+      return;
+    }
+    const size_t per = ((bytes + parts - 1) / parts + 63) & ~size_t(63);
+    std::unique_lock<std::mutex> lk(mu_);
+    pending_ = 0;
+    for (int i = 1; i < parts; ++i) {
+      const size_t off = per * i;
+      if (off >= bytes) break;
+      const size_t len = std::min(per, bytes - off);
+      ++pending_;
+      jobs_.push_back([=] { std::memcpy((char*)dst + off, (const char*)src + off, len); });
+    }
+    lk.unlock();
+    cv_.notify_all();
+    std::memcpy(dst, src, std::min(per, bytes));
+    lk.lock();
+    done_.wait(lk, [this] { return pending_ == 0; });
+  }
+
+ private:
+  void loop() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [this] { return stop_ || !jobs_.empty(); });
+      if (stop_) return;
+      auto job = std::move(jobs_.back());
+      jobs_.pop_back();
+      lk.unlock();
+      job();
+      lk.lock();
+      if (--pending_ == 0) done_.notify_all();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::vector<std::function<void()>> jobs_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  int pending_ = 0;
+  bool stop_ = false;
+};
+
+struct PinRing {
+  char* p[kPinSlots] = {};
+  hipEvent_t ev[kPinSlots] = {};
+  CopyPool* pool = nullptr;
+};
+
 }  // namespace
 
 struct jwv_ctx {
@@ -53,7 +134,8 @@ struct jwv_ctx {
   DevBuf big;    // full-size intermediate between 2-D/3-D axes
   DevBuf big2;   // full-size intermediate between multi-pass WPT passes
   DevBuf red;    // reduction scratch (CompressorMagnitude)
-  DevBuf hin, hout;  // staging for the host-pointer entry points
+  DevBuf hin, hout;  // device buffers of the host-pointer entry points
+  PinRing pin;       // their pinned host staging (allocated on first use)
   // single-launch FWT chains: [0, kWords) forward counters, [kWords, 2 kWords)
   // reverse ticket/flags; zeroed once, left zero by every completed launch
   unsigned* sync = nullptr;
@@ -700,15 +782,83 @@ void check_waits(jwv_ctx* c) {
   }
 }
 
+// Page-locked host memory (hipHostMalloc / hipHostRegister): DMA-able as is.
+bool host_pinned(const void* p) {
+  hipPointerAttribute_t at{};
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();  // plain pageable memory
+    return false;
+  }
+  return at.type == hipMemoryTypeHost;
+}
+
+PinRing& pin_ring(jwv_ctx* c) {
+  PinRing& r = c->pin;
+  if (!r.p[0]) {
+    for (int i = 0; i < kPinSlots; ++i) {
+      hipchk(hipHostMalloc((void**)&r.p[i], kPinChunk, hipHostMallocDefault), "hipHostMalloc");
+      hipchk(hipEventCreateWithFlags(&r.ev[i], hipEventDisableTiming), "hipEventCreate");
+    }
+    const int hw = (int)std::thread::hardware_concurrency();
+    r.pool = new CopyPool(std::max(0, std::min(hw, 8) - 1));
+  }
+  return r;
+}
+
+// host x -> device dx (queued on the stream; returns when x may be reused)
+void copy_in(jwv_ctx* c, const double* x, double* dx, size_t n) {
+  const size_t bytes = n * sizeof(double);
+  if (host_pinned(x)) {
+    hipchk(hipMemcpyAsync(dx, x, bytes, hipMemcpyHostToDevice, c->stream), "H2D");
+    return;
+  }
+  PinRing& r = pin_ring(c);
+  for (size_t off = 0, k = 0; off < bytes; off += kPinChunk, ++k) {
+    const int s = (int)(k % kPinSlots);
+    const size_t len = std::min(kPinChunk, bytes - off);
+    hipchk(hipEventSynchronize(r.ev[s]), "staging slot");  // its previous DMA is done
+    r.pool->copy(r.p[s], (const char*)x + off, len);
+    hipchk(hipMemcpyAsync((char*)dx + off, r.p[s], len, hipMemcpyHostToDevice, c->stream), "H2D");
+    hipchk(hipEventRecord(r.ev[s], c->stream), "hipEventRecord");
+  }
+}
+
+// device dy -> host y, after the queued work; returns when y is complete
+void copy_out(jwv_ctx* c, const double* dy, double* y, size_t n) {
+  const size_t bytes = n * sizeof(double);
+  if (host_pinned(y)) {
+    hipchk(hipMemcpyAsync(y, dy, bytes, hipMemcpyDeviceToHost, c->stream), "D2H");
+    hipchk(hipStreamSynchronize(c->stream), "sync");
+    return;
+  }
+  PinRing& r = pin_ring(c);
+  const size_t nk = (bytes + kPinChunk - 1) / kPinChunk;
+  auto issue = [&](size_t k) {
+    const int s = (int)(k % kPinSlots);
+    const size_t off = k * kPinChunk, len = std::min(kPinChunk, bytes - off);
+    hipchk(hipMemcpyAsync(r.p[s], (const char*)dy + off, len, hipMemcpyDeviceToHost, c->stream),
+           "D2H");
+    hipchk(hipEventRecord(r.ev[s], c->stream), "hipEventRecord");
+  };
+  for (size_t k = 0; k < std::min<size_t>(nk, kPinSlots); ++k) issue(k);
+  for (size_t k = 0; k < nk; ++k) {
+    const int s = (int)(k % kPinSlots);
+    const size_t off = k * kPinChunk, len = std::min(kPinChunk, bytes - off);
+    hipchk(hipEventSynchronize(r.ev[s]), "staging slot");
+    r.pool->copy((char*)y + off, r.p[s], len);
+    if (k + kPinSlots < nk) issue(k + kPinSlots);
+  }
+  hipchk(hipStreamSynchronize(c->stream), "sync");
+}
+
 // Host-pointer wrapper: stage in / run device body / stage out, synchronous.
 template <typename Body>
 void staged(jwv_ctx* c, const double* x, size_t nx, double* y, size_t ny, Body&& body) {
   double* dx = grow(c, c->hin, nx);
   double* dy = grow(c, c->hout, ny);
-  hipchk(hipMemcpyAsync(dx, x, nx * sizeof(double), hipMemcpyHostToDevice, c->stream), "H2D");
+  copy_in(c, x, dx, nx);
   body(dx, dy);
-  hipchk(hipMemcpyAsync(y, dy, ny * sizeof(double), hipMemcpyDeviceToHost, c->stream), "D2H");
-  hipchk(hipStreamSynchronize(c->stream), "sync");
+  copy_out(c, dy, y, ny);
   check_waits(c);
 }
 
@@ -1125,11 +1275,15 @@ int jwv_ctx_create(int device, jwv_ctx** out) {
                    std::string("no HIP device available: ") + hipGetErrorString(e));
   if (device < 0 || device >= count)
     return set_err(nullptr, JWV_ERR_BAD_CALL, "device index out of range");
+  int prev = -1;
+  if (hipGetDevice(&prev) != hipSuccess) prev = -1;
   if ((e = hipSetDevice(device)) != hipSuccess)
     return set_err(nullptr, JWV_ERR_DEVICE, hipGetErrorString(e));
   jwv_ctx* c = new jwv_ctx();
   c->device = device;
-  if ((e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking)) != hipSuccess) {
+  e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking);
+  if (prev >= 0 && prev != device) (void)hipSetDevice(prev);  // the caller's device
+  if (e != hipSuccess) {
     delete c;
     return set_err(nullptr, JWV_ERR_DEVICE, hipGetErrorString(e));
   }
@@ -1138,8 +1292,25 @@ int jwv_ctx_create(int device, jwv_ctx** out) {
   return JWV_OK;
 }
 
+int jwv_host_alloc(jwv_ctx* c, int64_t bytes, void** p) {
+  return guarded(c, [&] {
+    if (!p || bytes < 0) throw Fail{JWV_ERR_BAD_CALL, "jwv_host_alloc: bad arguments"};
+    *p = nullptr;
+    hipchk(hipHostMalloc(p, (size_t)std::max<int64_t>(bytes, 1), hipHostMallocDefault),
+           "hipHostMalloc");
+  });
+}
+
+int jwv_host_free(jwv_ctx* c, void* p) {
+  return guarded(c, [&] {
+    if (p) hipchk(hipHostFree(p), "hipHostFree");
+  });
+}
+
 int jwv_ctx_destroy(jwv_ctx* c) {
   if (!c) return JWV_OK;
+  int prev = -1;
+  if (hipGetDevice(&prev) != hipSuccess) prev = -1;
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->ws[0], &c->ws[1], &c->big, &c->big2, &c->red, &c->hin, &c->hout})
@@ -1147,8 +1318,14 @@ int jwv_ctx_destroy(jwv_ctx* c) {
   if (c->sync) hipFree(c->sync);
   for (auto& r : c->recs) { hipEventDestroy(r.e0); hipEventDestroy(r.e1); }
   for (auto e : c->ev_pool) hipEventDestroy(e);
+  for (int i = 0; i < kPinSlots; ++i) {
+    if (c->pin.p[i]) hipHostFree(c->pin.p[i]);
+    if (c->pin.ev[i]) hipEventDestroy(c->pin.ev[i]);
+  }
+  delete c->pin.pool;
   if (c->own) hipStreamDestroy(c->own);
   delete c;
+  if (prev >= 0) hipSetDevice(prev);
   return JWV_OK;
 }
 

@@ -41,7 +41,11 @@ struct Fwd1Geo {
 #ifndef JWV_FWD_FENCE_MINL
 #define JWV_FWD_FENCE_MINL 12
 #endif
-template <int L, int NT, int T, int K, bool FMA, int l, bool WT = false>
+// CP: a lane computes two adjacent pairs ("a couple", L+2 window values read
+// as 16-B LDS reads at a 32-B lane stride, 2-way bank-conflicted on
+// ds_read_b128); !CP: one pair per lane, L values read at a 16-B lane stride
+// (conflict-free), 8-B output stores.
+template <int L, int NT, int T, int K, bool FMA, int l, bool WT = false, bool CP = true>
 struct Fwd1Level {
   // level l reads the level-(l-1) window at lds + off(l-1) (l = 1: lds) and
   // writes its approximations at lds + off(l) (the last level: ya).
@@ -61,6 +65,47 @@ struct Fwd1Level {
     double* out = lds + G::off(l);
     const int tid = opaque_tid();  // per-level: keeps address math out of the prologue
     double* __restrict__ yd = yd0 + (hl >> 1) + (int64_t)t * own;
+    if constexpr (!CP) {
+      constexpr int RS = (mo + NT - 1) / NT;
+      double as[RS];
+#pragma unroll
+      for (int r = 0; r < RS; ++r) {
+        const int p = tid + r * NT;
+        if ((r + 1) * NT <= mo || p < mo) {
+          double x[L];
+#pragma unroll
+          for (int j = 0; j < L; j += 2) {
+            const double2 v = *reinterpret_cast<const double2*>(in + 2 * p + j);
+            x[j] = v.x;
+            x[j + 1] = v.y;
+          }
+          double a, d;
+          fwd_pair<L, FMA>(tp, [&](int j) { return x[j]; }, a, d);
+          if constexpr (l == K) {
+            if constexpr (WT) st_wt(ya + (int64_t)t * own + p, a);
+            else ya[(int64_t)t * own + p] = a;
+          } else if constexpr (l == 1) {
+            as[r] = a;
+          } else {
+            out[p] = a;
+          }
+          if (r * NT < own && ((r + 1) * NT <= own || p < own)) yd[p] = d;
+        }
+      }
+      if constexpr (l < K) {
+        if constexpr (l == 1) {
+          lds_barrier();
+#pragma unroll
+          for (int r = 0; r < RS; ++r) {
+            const int p = tid + r * NT;
+            if ((r + 1) * NT <= mo || p < mo) out[p] = as[r];
+          }
+        }
+        lds_barrier();
+        Fwd1Level<L, NT, T, K, FMA, l + 1, WT, CP>::run(tp, lds, yd0, hl >> 1, t, ya, sp);
+      }
+      return;
+    }
     double2 av[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -107,7 +152,7 @@ struct Fwd1Level {
         }
       }
       lds_barrier();
-      Fwd1Level<L, NT, T, K, FMA, l + 1, WT>::run(tp, lds, yd0, hl >> 1, t, ya, sp);
+      Fwd1Level<L, NT, T, K, FMA, l + 1, WT, CP>::run(tp, lds, yd0, hl >> 1, t, ya, sp);
     }
   }
 };
@@ -115,7 +160,7 @@ struct Fwd1Level {
 // Grid: nouter * (h / T) blocks, tile-fastest, XCD-remapped like fwt_fwd_tile.
 // src: level input (length h, stride 1); dst: coefficient array of the
 // signal (details of level size hl at dst[hl/2 ..]); adst: level-K output.
-template <int L, int NT, int T, int K, bool FMA>
+template <int L, int NT, int T, int K, bool FMA, bool CP = true>
 __global__ __launch_bounds__(NT) void fwt_fwd_tile1(const double* __restrict__ src,
                                                     int64_t s_src, double* __restrict__ dst,
                                                     int64_t s_dst, double* __restrict__ adst,
@@ -135,7 +180,8 @@ __global__ __launch_bounds__(NT) void fwt_fwd_tile1(const double* __restrict__ s
                                           [&](int e) { return (int64_t)((base + e) & msk); });
   dma_fence_barrier();
   JWV_STAMP(1);
-  Fwd1Level<L, NT, T, K, FMA, 1>::run(tp, lds, dst + o * s_dst, h, t, adst + o * s_adst, sp);
+  Fwd1Level<L, NT, T, K, FMA, 1, false, CP>::run(tp, lds, dst + o * s_dst, h, t, adst + o * s_adst,
+                                                 sp);
 }
 
 // ---------------------------------------------------------------- reverse

@@ -859,3 +859,46 @@ def test_fwt_denoise(ctx, wname, n, lev):
     assert_exact(jw.fwt_denoise(x, w, lev, 1.5, ctx), ref, "denoise")
     yd = jw.fwt_denoise(torch.from_numpy(x).cuda(), w, lev, 1.5, ctx)
     assert_exact(yd.cpu().numpy(), ref, "denoise device")
+
+
+def test_host_entry_staging_paths(ctx):
+    """The host-pointer entries (Transform.forward(double[]) semantics) move
+    pageable arrays through the pinned staging ring in 8 MiB chunks and DMA
+    page-locked arrays (jwv_host_alloc) directly: every combination gives the
+    device entry's bits, for sizes that end mid-chunk, and the caller's
+    current device is left as it was."""
+    import ctypes
+    import torch
+    from jwave_amd import _lib as L
+    from jwave_amd.transforms import _TapsHolder
+    lib = L.lib()
+    w = jw.by_class("Daubechies4")
+    t = _TapsHolder.of(w)
+    for n, lev in ((1 << 22, 22), ((1 << 20) * 3, 0), (1 << 10, 10)):
+        if lev == 0:  # 3 Mi doubles (not a power of two): AED path of one call
+            x = rnd(n, 5)
+            ref = T.aed_transform(torch.from_numpy(x).cuda(), w, "fwt", True, ctx).cpu().numpy()
+            got = T.aed_transform(x, w, "fwt", True, ctx)
+            assert_exact(got, ref, "aed host entry n=%d" % n)
+            continue
+        x = rnd(n, 3)
+        ref = T.fwt_forward(torch.from_numpy(x).cuda(), w, lev, ctx).cpu().numpy()
+        assert_exact(T.fwt_forward(x, w, lev, ctx), ref, "pageable n=%d" % n)
+        pin = [ctypes.c_void_p(), ctypes.c_void_p()]
+        for p in pin:
+            assert lib.jwv_host_alloc(ctx.handle, n * 8, ctypes.byref(p)) == 0
+        try:
+            px = np.ctypeslib.as_array((ctypes.c_double * n).from_address(pin[0].value))
+            py = np.ctypeslib.as_array((ctypes.c_double * n).from_address(pin[1].value))
+            px[:] = x
+            dp = ctypes.POINTER(ctypes.c_double)
+            for src, dst in ((px, py), (px, np.empty(n)), (x, py)):
+                dst[:] = np.nan
+                rc = lib.jwv_fwt_fwd_f64(src.ctypes.data_as(dp), dst.ctypes.data_as(dp), n, lev,
+                                         t, ctx.handle)
+                assert rc == 0, lib.jwv_last_error(ctx.handle)
+                assert_exact(dst, ref, "pinned/pageable mix n=%d" % n)
+        finally:
+            for p in pin:
+                assert lib.jwv_host_free(ctx.handle, p) == 0
+    assert torch.cuda.current_device() == 0
