@@ -403,14 +403,20 @@ def load_traffic(workload, kernel, math):
     return None, None
 
 
-def timed(d, step, steps):
+def timed(d, step, steps, issue=None):
+    """Seconds for `steps` steps between barrier + device syncs; `issue`
+    (a list) receives the host time spent enqueueing them (when it is close
+    to the total, the host, not the GPU, sets the pace)."""
     d.barrier()
     d.sync()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
+    t1 = time.perf_counter()
     d.sync()
     d.barrier()
+    if issue is not None:
+        issue.append(t1 - t0)
     return time.perf_counter() - t0
 
 
@@ -554,7 +560,8 @@ def main():
         kname = max(pre.items(), key=lambda kv: kv[1]["total_ms"])[0]
 
     # timed region A: the metric (no events)
-    el = d.max(timed(d, step, args.steps))
+    issue = []
+    el = d.max(timed(d, step, args.steps, issue))
 
     out_roof, out_fp64, tb = None, None, None
     if ctx is not None:
@@ -597,6 +604,7 @@ def main():
     out = {"metric": W["metric"], "value": round(value, 1), "unit": "samples/s",
            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True,
+           "host_issue_ms_per_step": round(issue[0] / args.steps * 1e3, 4),
            "scaling": W["scaling"], "vs_baseline": None,
            "dtype": "f64", "data": "synthetic (uniform [0,1) doubles, seed 42+rank)",
            "config": W["config"], "hbm_gbps": round(gbps, 1), "roofline": out_roof,

@@ -472,7 +472,8 @@ void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
     const AxisView av = last ? a.dv : cview(h >> K, a.inner);
     jwv::TileArgs t{cur, cv, nullptr, {}, a.dst, a.dv, ad, av, h, K, a.outer, a.inner,
                     dma_view(cur, cv, C, a.inner),
-                    h == a.len ? Geo::store_pol() | (a.outer == 1 ? Geo::tile_desc(0) : 0) : 0,
+                    (h == a.len ? Geo::store_pol() | (a.outer == 1 ? Geo::tile_desc(0) : 0) : 0) |
+                        Geo::tile_walk(),
                     first1 && h == a.len && Geo::fwd1_first_t() != Geo::kFwt1T
                         ? Geo::fwd1_first_t() : 0};
     { ProfScope ps_(c, h == a.len ? K_FWT_FWD_TILE : K_FWT_FWD_TILE_DEEP,
@@ -576,7 +577,8 @@ void fwt_rev_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
     const AxisView ov = last ? a.dv : cview(hK, a.inner);
     jwv::TileArgs t{acur, acv, a.src, a.sv, out, ov, nullptr, {}, h1, K, a.outer, a.inner,
                     dma_view(acur, acv, C, a.inner) && dma_view(a.src, a.sv, C, a.inner),
-                    last ? Geo::store_pol() | (a.outer == 1 ? Geo::tile_desc(1) : 0) : 0};
+                    (last ? Geo::store_pol() | (a.outer == 1 ? Geo::tile_desc(1) : 0) : 0) |
+                        Geo::tile_walk()};
     { ProfScope ps_(c, last ? K_FWT_REV_TILE : K_FWT_REV_TILE_DEEP, 16.0 * a.outer * hK * a.inner);
     hipchk(jwv::launch_fwt_rev_tile(b, use_fma(c), C, t, c->stream), "fwt_rev_tile"); }
     acur = out;
@@ -1149,6 +1151,20 @@ int Geo::store_pol() {
 int Geo::tile_desc(int rev) {
   static const int d = env_int("JWV_TILE_DESC", 0);
   return ((d >> rev) & 1) << 2;
+}
+// Default G = 64 (config 2, one MI355X, alternating runs on one box: forward
+// big pass 53.7 -> 46.0 us by rocprofv3, 0.1231-0.1256 -> 0.1146-0.1182
+// ms/step; G = 32 / 128 within noise of 64; JWV_TILE_G=0 restores the
+// chunked walk).
+int Geo::tile_walk() {
+  static const int w = [] {
+    const int g = env_int("JWV_TILE_G", 64);
+    if (g <= 0 || (g & (g - 1)) || g > (1 << 20)) return 0;
+    int gs = 0;
+    while ((1 << gs) < g) ++gs;
+    return 8 | (gs << 8);
+  }();
+  return w;
 }
 int Geo::fwd1_first_t() {
   static const int t = env_int("JWV_FWD1T", kFwt1T) == 1024 ? 1024 : kFwt1T;

@@ -257,10 +257,20 @@ typedef unsigned int jwv_u32x4 __attribute__((ext_vector_type(4)));
 // (its L2 keeps the halo rows); sp bit 2 walks every chunk last-to-first
 // (the next pass then starts on the most recently written, MALL-resident
 // end).  Clears the bit (st2_pol reads sp & 3).
+// sp bit 3 selects the grouped walk instead: XCD x takes groups of G = 2^(sp
+// bits 8..12) consecutive tiles and the 8 XCDs work side by side, so the grid
+// sweeps memory as ONE front (the chunked walk runs 8 fronts exactly 1/8 of
+// the array apart, which cold HBM serves more slowly).
 __device__ __forceinline__ int tile_order(int nblk, int& sp) {
   const bool desc = (sp & 4) != 0;
+  const bool grouped = (sp & 8) != 0;
+  const int gs = (sp >> 8) & 31;
   sp &= 3;
   const int b = blockIdx.x;
+  if (grouped && (nblk & ((8 << gs) - 1)) == 0) {
+    const int x = b & 7, j = b >> 3;
+    return ((j >> gs) << (gs + 3)) + (x << gs) + (j & ((1 << gs) - 1));
+  }
   if ((nblk & 7) == 0) {
     const int per = nblk >> 3, j = b >> 3;
     return (b & 7) * per + (desc ? per - 1 - j : j);

@@ -105,6 +105,10 @@ struct Geo {
   // JWV_STPOL (0 plain, 1 sc1, 2 nt)
   static int store_pol();
   static int tile_desc(int rev);  // sp bit 2 for the big pass (env JWV_TILE_DESC)
+  // sp bits of the C = 1 tile walk (tile_order): the grouped one-front walk
+  // with G = 64 tiles per XCD group (env JWV_TILE_G = G, a power of two;
+  // 0 = the XCD-chunked walk)
+  static int tile_walk();
   // First (full-length) forward pass of one long contiguous signal: tile
   // (2048 | 1024, env JWV_FWD1T) and fused levels (env JWV_FWD1K); the last
   // forward tile pass runs down to fwd1_tail() samples (env JWV_FWD1TAIL).
