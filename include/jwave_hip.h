@@ -87,10 +87,14 @@ int jwv_ctx_set_math(jwv_ctx* ctx, int mode);
  * launch (no inter-workgroup wait: every block recomputes the resident part);
  * JWV_PLAN_CHAIN_REV / _FWD: the whole reverse / forward in one launch (the
  * reverse chain has bounded in-kernel waits, see jwv_ctx_synchronize).
+ * JWV_PLAN_FWD_TAIL: the forward's deep tiled pass and its resident pass in
+ * one launch (the unit that completes an arrival counter runs the resident
+ * levels; no wait).
  * Default: JWV_PLAN_REV_HEAD (env JWV_PLAN overrides the default flags). */
 #define JWV_PLAN_CHAIN_REV 1
 #define JWV_PLAN_CHAIN_FWD 2
 #define JWV_PLAN_REV_HEAD 4
+#define JWV_PLAN_FWD_TAIL 8
 int jwv_ctx_set_plan(jwv_ctx* ctx, int flags);
 /* Waits for the context's stream.  Also reports (JWV_ERR_DEVICE) a chained
  * launch whose bounded in-kernel wait gave up since the last check (its results

@@ -26,6 +26,7 @@ JWV_MATH_FMA = 1
 JWV_PLAN_CHAIN_REV = 1
 JWV_PLAN_CHAIN_FWD = 2
 JWV_PLAN_REV_HEAD = 4
+JWV_PLAN_FWD_TAIL = 8
 JWV_TRANSFORM_FWT = 0
 JWV_TRANSFORM_WPT = 1
 

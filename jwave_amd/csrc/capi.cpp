@@ -236,7 +236,7 @@ enum KernelKind {
   K_FWT_FWD_TILE, K_FWT_FWD_RES, K_FWT_REV_TILE, K_FWT_REV_RES, K_WPT_FWD_TILE, K_WPT_FWD_RES,
   K_WPT_REV_TILE, K_WPT_REV_RES, K_MODWT_FWD_TILE, K_MODWT_FWD_LEVEL, K_MODWT_INV_TILE,
   K_MODWT_INV_LEVEL, K_COPY, K_FWT_FWD_CHAIN, K_FWT_REV_CHAIN, K_FWT_REV_HEAD,
-  K_FWT_FWD_TILE_DEEP, K_FWT_REV_TILE_DEEP, K_AED_VARLEN, K_NKINDS
+  K_FWT_FWD_TILE_DEEP, K_FWT_REV_TILE_DEEP, K_AED_VARLEN, K_FWT_FWD_TAIL, K_NKINDS
 };
 // *_tile: the tiled pass that reads (forward) or writes (reverse) the full-length
 // axis — the HBM-bound launch; *_tile_deep: tiled passes over an intermediate
@@ -246,7 +246,7 @@ const char* const kKindNames[K_NKINDS] = {
     "fwt_fwd_tile", "fwt_fwd_res", "fwt_rev_tile", "fwt_rev_res", "wpt_fwd_tile", "wpt_fwd_res",
     "wpt_rev_tile", "wpt_rev_res", "modwt_fwd_tile", "modwt_fwd_level", "modwt_inv_tile",
     "modwt_inv_level", "copy_axis", "fwt_fwd_chain", "fwt_rev_chain", "fwt_rev_head",
-    "fwt_fwd_tile_deep", "fwt_rev_tile_deep", "aed_varlen"};
+    "fwt_fwd_tile_deep", "fwt_rev_tile_deep", "aed_varlen", "fwt_fwd_tail"};
 
 hipEvent_t take_event(jwv_ctx* c) {
   if (!c->ev_pool.empty()) {
@@ -357,8 +357,10 @@ using jwv::ChainGeo;
 
 unsigned* sync_words(jwv_ctx* c) {
   if (!c->sync) {
-    HIPCHK(hipMalloc(&c->sync, 2 * ChainGeo::kWords * sizeof(unsigned)));
-    HIPCHK(hipMemsetAsync(c->sync, 0, 2 * ChainGeo::kWords * sizeof(unsigned), c->stream));
+    // [0, kWords) forward chain, [kWords, 2 kWords) reverse chain, then the
+    // fused forward tail's counter (kTailWord)
+    HIPCHK(hipMalloc(&c->sync, (2 * ChainGeo::kWords + 16) * sizeof(unsigned)));
+    HIPCHK(hipMemsetAsync(c->sync, 0, (2 * ChainGeo::kWords + 16) * sizeof(unsigned), c->stream));
   }
   return c->sync;
 }
@@ -422,6 +424,22 @@ int fwt_res_cap(int C, int64_t outer) {
   return Geo::res_cap(C);
 }
 
+// Cache policy of the full-length output stores of the forward (rev = 0) and
+// reverse (rev = 1) big passes (st2_pol: 0 plain, 1 sc1, 2 nt): env
+// JWV_STPOL_F / JWV_STPOL_R, else JWV_STPOL.
+int store_pol_dir(int rev) {
+  static const int p[2] = {[] {
+                             const char* e = std::getenv("JWV_STPOL_F");
+                             return e ? std::atoi(e) : Geo::store_pol();
+                           }(),
+                           [] {
+                             const char* e = std::getenv("JWV_STPOL_R");
+                             return e ? std::atoi(e) : Geo::store_pol();
+                           }()};
+  const int v = p[rev & 1];
+  return v < 0 || v > 2 ? 0 : v;
+}
+
 // env JWV_FWD1S (default 0): the first forward pass of contiguous signals on
 // the persistent grid of fwt1_stream.hpp instead of one block per tile
 bool fwd_stream1() {
@@ -467,12 +485,24 @@ void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
   int h = a.len, rem = nlev, pp = 0;
   while (rem > 0 && h > cap) {
     const int K = pick_k(h, rem);
+    // JWV_PLAN_FWD_TAIL: this deep pass and the resident remainder in one
+    // launch (fwt_fwd_tail1)
+    if (f1 && a.outer == 1 && h < a.len && (plan_of(c) & JWV_PLAN_FWD_TAIL) &&
+        K >= jwv::kTailKMin && K <= jwv::kTailKMax && rem > K && h % jwv::kTailTB == 0 &&
+        (h >> K) <= jwv::kTailCap && ((uintptr_t)cur & 15) == 0) {
+      jwv::TailArgs ta{cur, a.dst, c->ws[pp].p, sync_words(c) + 2 * ChainGeo::kWords, h, K,
+                       rem - K};
+      { ProfScope ps_(c, K_FWT_FWD_TAIL, 16.0 * h);
+        hipchk(use_fma(c) ? jwv::fused::fwt_fwd_tail(b, ta, c->stream)
+                          : jwv::exact::fwt_fwd_tail(b, ta, c->stream), "fwt_fwd_tail"); }
+      return;
+    }
     const bool last = K == rem;
     double* ad = last ? a.dst : c->ws[pp].p;
     const AxisView av = last ? a.dv : cview(h >> K, a.inner);
     jwv::TileArgs t{cur, cv, nullptr, {}, a.dst, a.dv, ad, av, h, K, a.outer, a.inner,
                     dma_view(cur, cv, C, a.inner),
-                    (h == a.len ? Geo::store_pol() | (a.outer == 1 ? Geo::tile_desc(0) : 0) : 0) |
+                    (h == a.len ? store_pol_dir(0) | (a.outer == 1 ? Geo::tile_desc(0) : 0) : 0) |
                         Geo::tile_walk(),
                     first1 && h == a.len && Geo::fwd1_first_t() != Geo::kFwt1T
                         ? Geo::fwd1_first_t() : 0};
@@ -577,7 +607,7 @@ void fwt_rev_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
     const AxisView ov = last ? a.dv : cview(hK, a.inner);
     jwv::TileArgs t{acur, acv, a.src, a.sv, out, ov, nullptr, {}, h1, K, a.outer, a.inner,
                     dma_view(acur, acv, C, a.inner) && dma_view(a.src, a.sv, C, a.inner),
-                    (last ? Geo::store_pol() | (a.outer == 1 ? Geo::tile_desc(1) : 0) : 0) |
+                    (last ? store_pol_dir(1) | (a.outer == 1 ? Geo::tile_desc(1) : 0) : 0) |
                         Geo::tile_walk()};
     { ProfScope ps_(c, last ? K_FWT_REV_TILE : K_FWT_REV_TILE_DEEP, 16.0 * a.outer * hK * a.inner);
     hipchk(jwv::launch_fwt_rev_tile(b, use_fma(c), C, t, c->stream), "fwt_rev_tile"); }
@@ -1199,7 +1229,7 @@ bool Geo::rev_pref() {
 #define JWV_MODE2(name, ...) \
   return fma ? fused::name(__VA_ARGS__) : exact::name(__VA_ARGS__)
 int ChainGeo::default_plan() {
-  static const int p = env_int("JWV_PLAN", JWV_PLAN_REV_HEAD) & 7;
+  static const int p = env_int("JWV_PLAN", JWV_PLAN_REV_HEAD) & 15;
   return p;
 }
 hipError_t launch_fwt_rev_head(const Bank& b, bool fma, const RevHeadArgs& a, hipStream_t s) {
@@ -1373,7 +1403,7 @@ int jwv_ctx_set_math(jwv_ctx* c, int mode) {
 
 int jwv_ctx_set_plan(jwv_ctx* c, int flags) {
   if (!c) return set_err(nullptr, JWV_ERR_BAD_CALL, "ctx is NULL");
-  if (flags & ~(JWV_PLAN_CHAIN_REV | JWV_PLAN_CHAIN_FWD | JWV_PLAN_REV_HEAD))
+  if (flags & ~(JWV_PLAN_CHAIN_REV | JWV_PLAN_CHAIN_FWD | JWV_PLAN_REV_HEAD | JWV_PLAN_FWD_TAIL))
     return set_err(c, JWV_ERR_BAD_CALL, "unknown plan flag");
   c->plan = flags;
   return JWV_OK;

@@ -68,7 +68,7 @@ class Context:
         if flags is None:
             flags = {"rev_head"}
         bits = {"chain_rev": L.JWV_PLAN_CHAIN_REV, "chain_fwd": L.JWV_PLAN_CHAIN_FWD,
-                "rev_head": L.JWV_PLAN_REV_HEAD}
+                "rev_head": L.JWV_PLAN_REV_HEAD, "fwd_tail": L.JWV_PLAN_FWD_TAIL}
         self._check(self._lib.jwv_ctx_set_plan(self.handle, sum(bits[f] for f in set(flags))))
 
     def set_poll_limit(self, spins=0):

@@ -113,7 +113,7 @@ def test_fwt_chain(ctx, wname, n):
     x = rnd(n, n + 1)
     full = n.bit_length() - 1
     try:
-        for plan in ({"rev_head"}, {"chain_rev", "chain_fwd"}, set()):
+        for plan in ({"rev_head"}, {"rev_head", "fwd_tail"}, {"chain_rev", "chain_fwd"}, set()):
             ctx.set_plan(plan)
             for lev in sorted({12, 13, 14, 15, full - 1, full}):
                 yr = oracle.fwt_forward(w, x, lev)
