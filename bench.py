@@ -154,10 +154,32 @@ class Dist:
 
 
 # ------------------------------------------------------------------ workloads
+class PlaceholderBackend:
+    """--dry-run per-rank "compute" on CPU tensors: copies of the right shapes,
+    so the sharded workloads' exchanges (jwave_amd.distributed: all-to-all
+    transposes, MODWT ring halos) run for real over gloo without a GPU."""
+
+    def rows(self, x, w, level, forward, kind="fwt"):
+        return x.clone()
+
+    def cols(self, x, w, level, forward, kind="fwt"):
+        return x.clone()
+
+    def modwt_fwd_ld(self, x, c, n, J, w):
+        c[:, :n] = x[:n]
+
+    def modwt_inv_ld(self, c, col0, n, x, w):
+        x[:n] = c[0, col0:col0 + n]
+
+
 def setup_dry(args, d):
     """--dry-run: a placeholder host step (no transform, no GPU) so the
-    launcher, barriers and max-over-ranks timing can be tested on CPU."""
+    launcher, barriers and max-over-ranks timing can be tested on CPU; the
+    sharded workloads (fwt2d, modwt at world > 1) run their real exchanges
+    around placeholder compute."""
     import numpy as np
+    if d.world > 1 and args.workload in ("fwt2d", "modwt"):
+        return setup_sharded(args, d, None, PlaceholderBackend(), "cpu", small=True)
     a = np.random.default_rng(d.rank).random(1 << 16)
     b = np.empty_like(a)
 
@@ -168,6 +190,75 @@ def setup_dry(args, d):
                 metric="dry-run (launcher test, no transform)",
                 config={"workload": "dry-run", "parallelism": "ranks x%d" % d.world},
                 scaling="weak", cpu=None)
+
+
+def setup_sharded(args, d, ctx, backend, device, small=False):
+    """Configs 3 and 5 split over the ranks as SURVEY 8(e) / DESIGN 7 shard
+    them (strong scaling: one problem, fixed total size):
+      fwt2d: row block per rank -> row pass -> all-to-all transpose -> column
+             pass on the [R][C/W] slab; the reverse mirrors it
+             (ParallelTransform.java:70-126's row/column structure);
+      modwt: contiguous slices of the 10^7-sample signal, one ring halo
+             exchange per direction (MODWTTransform.java:256-375).
+    'exchange' times the data-path collectives alone on the same buffers."""
+    import numpy as np
+    import torch
+    from jwave_amd import distributed as D
+    import jwave_amd as jw
+    W, rank = d.world, d.rank
+    if args.workload == "fwt2d":
+        r = c = 256 if small else 8192
+        lev = r.bit_length() - 1
+        w = jw.by_class("Daubechies8") if small else d.broadcast_taps("Daubechies8")
+        rw = r // W
+        full = np.random.default_rng(42).random((r, c))
+        x = torch.from_numpy(np.ascontiguousarray(full[rank * rw:(rank + 1) * rw])).to(device)
+        del full
+        st = {}
+
+        def step():
+            slab = D.forward_2d(x, r, c, w, lev, lev, backend)
+            st["xr"] = D.reverse_2d(slab, r, c, w, lev, lev, backend)
+
+        a = torch.empty((rw, c), dtype=torch.float64, device=device)
+        b = torch.empty((r, c // W), dtype=torch.float64, device=device)
+
+        def exchange():
+            D._transpose_rows_to_cols(a, W, None)
+            D._transpose_cols_to_rows(b, W, None)
+
+        return dict(ctx=ctx, step=step, exchange=exchange,
+                    check=lambda: float((st["xr"] - x).abs().max().item()),
+                    samples=2 * rw * c, bytes=2 * 32.0 * rw * c,
+                    metric="samples/s, 2D FWT Daubechies8 8192x8192 fp64",
+                    config={"workload": "fwt2d: 2D FWT Daubechies8 %dx%d, %dx%d levels, "
+                                        "forward+reverse per step, row blocks -> all-to-all -> "
+                                        "column slabs" % (r, c, lev, lev), "math": args.math,
+                            "parallelism": "sharded x%d (strong)" % W},
+                    scaling="strong", cpu=None if small else ("fwt2d", w))
+    n, J = (20_000 if small else 10_000_000), 8
+    w = jw.by_class("Daubechies4") if small else d.broadcast_taps("Daubechies4")
+    sh = D.ModwtShard(n, w, J, device)
+    xs = np.random.default_rng(42).random(n)[sh.start:sh.start + sh.n]
+    sh.x.copy_(torch.from_numpy(xs).to(device))
+
+    def step():
+        sh.forward(backend)
+        sh.inverse(backend)
+
+    def exchange():
+        sh.exchange_forward()
+        sh.exchange_inverse()
+
+    return dict(ctx=ctx, step=step, exchange=exchange,
+                check=lambda: float((sh.xr[:sh.n] - sh.x).abs().max().item()),
+                samples=2 * sh.n, bytes=2 * 80.0 * sh.n,
+                metric="samples/s, MODWT Daubechies4 J=8 N=1e7 fp64",
+                config={"workload": "modwt: Daubechies4, J=8, N=%d, forwardMODWT+inverseMODWT "
+                                    "per step, contiguous slices + ring halo (%d samples)"
+                                    % (n, sh.H), "math": args.math,
+                        "parallelism": "sharded x%d (strong)" % W},
+                scaling="strong", cpu=None if small else ("modwt", w))
 
 
 def setup(args, d, workload=None):
@@ -218,6 +309,10 @@ def setup(args, d, workload=None):
                             "directions_per_step": 2, "math": args.math,
                             "parallelism": "replicas x%d (one signal per GPU)" % d.world},
                     scaling="weak", cpu=("fwt1d", w))
+    if workload in ("fwt2d", "modwt") and d.world > 1:
+        from jwave_amd import distributed as D
+        args.workload = workload
+        return setup_sharded(args, d, ctx, D.HipBackend(ctx), d.dev)
     if workload == "fwt2d":
         r = c = 8192
         w = d.broadcast_taps("Daubechies8")
@@ -595,6 +690,11 @@ def main():
                         "flops_per_launch": fl,
                         "exact_mode_ceiling": FP64_PEAK_TFLOPS / 2 if args.math == "exact" else None}
 
+    exch = None
+    if W.get("exchange"):
+        # the data-path collectives of the sharded step alone, same buffers
+        W["exchange"]()
+        exch = d.max(timed(d, W["exchange"], args.steps)) / args.steps * 1e3
     world = d.world
     value = W["samples"] * args.steps * world / el
     gbps = W["bytes"] * args.steps * world / el / 1e9
@@ -614,6 +714,8 @@ def main():
         out["build"] = _lib.provenance()  # the library measured: its sources and digest
     if tb is not None:
         out["ms_per_step_with_events"] = round(tb / args.steps * 1e3, 4)
+    if exch is not None:
+        out["exchange_ms_per_step"] = round(exch, 4)
     if out_fp64:
         out["roofline_fp64"] = out_fp64
     if (not args.dry_run and args.workload == "fwt1d" and not args.no_secondary):

@@ -293,6 +293,14 @@ int jwv_modwt_fwd_f64_dev(const double* x, double* wv, int64_t n, int J, const j
                           jwv_ctx* ctx);
 int jwv_modwt_inv_f64_dev(const double* wv, double* x, int64_t n, int J, const jwv_taps* t,
                           jwv_ctx* ctx);
+/* The same on coefficient rows at a stride ldw >= n doubles (row j at
+ * wv + j*ldw): the sharded MODWT (jwave_amd/distributed.py) keeps a slice's
+ * rows between halo columns and transforms them in place of a packed copy.
+ * No reference counterpart (the reference's double[][] rows are ldw = n). */
+int jwv_modwt_fwd_ld_f64_dev(const double* x, double* wv, int64_t ldw, int64_t n, int J,
+                             const jwv_taps* t, jwv_ctx* ctx);
+int jwv_modwt_inv_ld_f64_dev(const double* wv, int64_t ldw, double* x, int64_t n, int J,
+                             const jwv_taps* t, jwv_ctx* ctx);
 /* The MODWT filters g, h (L doubles each) the engine derives from t
  * (MODWTTransform.initializeFilterCache :452-484). Host-only, no device. */
 int jwv_modwt_filters(const jwv_taps* t, double* g, double* h);

@@ -1069,7 +1069,10 @@ int64_t modwt_halo(int L, int j0, int j1) {
   return (int64_t)(L - 1) * ((int64_t(1) << j1) - (int64_t(1) << (j0 - 1)));
 }
 
-void body_modwt_fwd(jwv_ctx* c, const Bank& b, const double* x, double* wv, int64_t N, int J) {
+// wv rows (W_1 .. W_J, V_J) at stride ldw >= N doubles (ldw = N: the packed
+// [J+1][N] layout of the reference's double[][]).
+void body_modwt_fwd(jwv_ctx* c, const Bank& b, const double* x, double* wv, int64_t N, int J,
+                    int64_t ldw) {
   if (N == 0) return;
   const Bank m = modwt_bank(b);
   grow(c, c->ws[0], (size_t)N);
@@ -1081,8 +1084,8 @@ void body_modwt_fwd(jwv_ctx* c, const Bank& b, const double* x, double* wv, int6
     while (j1 + 1 <= J && modwt_halo(m.L, j0, j1 + 1) <= Geo::kModS) ++j1;
     const bool tiled = j1 >= j0;
     if (!tiled) j1 = j0;
-    double* vout = (j1 == J) ? wv + (int64_t)J * N : c->ws[pp].p;
-    jwv::ModwtArgs a{vin, nullptr, wv, vout, N, N, j0, j1};
+    double* vout = (j1 == J) ? wv + (int64_t)J * ldw : c->ws[pp].p;
+    jwv::ModwtArgs a{vin, nullptr, wv, vout, ldw, N, j0, j1};
     {
       ProfScope ps_(c, tiled ? K_MODWT_FWD_TILE : K_MODWT_FWD_LEVEL,
                     8.0 * N * (1 + (j1 - j0 + 1) + 1));
@@ -1094,12 +1097,13 @@ void body_modwt_fwd(jwv_ctx* c, const Bank& b, const double* x, double* wv, int6
   }
 }
 
-void body_modwt_inv(jwv_ctx* c, const Bank& b, const double* wv, double* x, int64_t N, int J) {
+void body_modwt_inv(jwv_ctx* c, const Bank& b, const double* wv, double* x, int64_t N, int J,
+                    int64_t ldw) {
   if (N == 0 || J < 1) return;
   const Bank m = modwt_bank(b);
   grow(c, c->ws[0], (size_t)N);
   grow(c, c->ws[1], (size_t)N);
-  const double* vin = wv + (int64_t)J * N;
+  const double* vin = wv + (int64_t)J * ldw;
   int pp = 0, j1 = J;
   while (j1 >= 1) {
     int j0 = j1 + 1;
@@ -1107,7 +1111,7 @@ void body_modwt_inv(jwv_ctx* c, const Bank& b, const double* wv, double* x, int6
     const bool tiled = j0 <= j1;
     if (!tiled) j0 = j1;
     double* vout = (j0 == 1) ? x : c->ws[pp].p;
-    jwv::ModwtArgs a{vin, wv, nullptr, vout, N, N, j0, j1};
+    jwv::ModwtArgs a{vin, wv, nullptr, vout, ldw, N, j0, j1};
     {
       ProfScope ps_(c, tiled ? K_MODWT_INV_TILE : K_MODWT_INV_LEVEL,
                     8.0 * N * (1 + (j1 - j0 + 1) + 1));
@@ -1812,7 +1816,7 @@ int jwv_modwt_fwd_f64(const double* x, double* wv, int64_t n, int J, const jwv_t
     if (n == 0) return;
     check_ptrs(x, wv);
     staged(c, x, (size_t)n, wv, (size_t)n * (J + 1),
-           [&](const double* dx, double* dy) { body_modwt_fwd(c, b, dx, dy, n, J); });
+           [&](const double* dx, double* dy) { body_modwt_fwd(c, b, dx, dy, n, J, n); });
   });
 }
 int jwv_modwt_fwd_f64_dev(const double* x, double* wv, int64_t n, int J, const jwv_taps* t,
@@ -1823,7 +1827,7 @@ int jwv_modwt_fwd_f64_dev(const double* x, double* wv, int64_t n, int J, const j
     if (n == 0) return;
     need_device_ptrs(c, x, wv);
     check_overlap(x, (size_t)n, wv, (size_t)n * (J + 1));
-    body_modwt_fwd(c, b, x, wv, n, J);
+    body_modwt_fwd(c, b, x, wv, n, J, n);
   });
 }
 // MODWTTransform.inverseMODWT: coefficients.length <= 1 -> empty (:338-346).
@@ -1835,7 +1839,7 @@ int jwv_modwt_inv_f64(const double* wv, double* x, int64_t n, int J, const jwv_t
     if (J > 13 || n > 0x7fffffffLL) throw Fail{JWV_ERR_BAD_CALL, "J > 13 or n too large"};
     check_ptrs(wv, x);
     staged(c, wv, (size_t)n * (J + 1), x, (size_t)n,
-           [&](const double* dx, double* dy) { body_modwt_inv(c, b, dx, dy, n, J); });
+           [&](const double* dx, double* dy) { body_modwt_inv(c, b, dx, dy, n, J, n); });
   });
 }
 int jwv_modwt_inv_f64_dev(const double* wv, double* x, int64_t n, int J, const jwv_taps* t,
@@ -1846,7 +1850,32 @@ int jwv_modwt_inv_f64_dev(const double* wv, double* x, int64_t n, int J, const j
     if (J > 13 || n > 0x7fffffffLL) throw Fail{JWV_ERR_BAD_CALL, "J > 13 or n too large"};
     need_device_ptrs(c, wv, x);
     check_overlap(wv, (size_t)n * (J + 1), x, (size_t)n);
-    body_modwt_inv(c, b, wv, x, n, J);
+    body_modwt_inv(c, b, wv, x, n, J, n);
+  });
+}
+
+int jwv_modwt_fwd_ld_f64_dev(const double* x, double* wv, int64_t ldw, int64_t n, int J,
+                             const jwv_taps* t, jwv_ctx* c) {
+  return guarded(c, [&] {
+    const Bank b = make_bank(t);
+    check_modwt(n, J);
+    if (n == 0) return;
+    if (ldw < n) throw Fail{JWV_ERR_BAD_CALL, "ldw < n"};
+    need_device_ptrs(c, x, wv);
+    check_overlap(x, (size_t)n, wv, (size_t)(J * ldw + n));
+    body_modwt_fwd(c, b, x, wv, n, J, ldw);
+  });
+}
+int jwv_modwt_inv_ld_f64_dev(const double* wv, int64_t ldw, double* x, int64_t n, int J,
+                             const jwv_taps* t, jwv_ctx* c) {
+  return guarded(c, [&] {
+    const Bank b = make_bank(t);
+    if (J < 1 || n == 0) return;
+    if (J > 13 || n > 0x7fffffffLL) throw Fail{JWV_ERR_BAD_CALL, "J > 13 or n too large"};
+    if (ldw < n) throw Fail{JWV_ERR_BAD_CALL, "ldw < n"};
+    need_device_ptrs(c, wv, x);
+    check_overlap(wv, (size_t)(J * ldw + n), x, (size_t)n);
+    body_modwt_inv(c, b, wv, x, n, J, ldw);
   });
 }
 

@@ -57,6 +57,16 @@ class HipBackend:
     def modwt_inv(self, c, w):
         return T.modwt_inverse(c, w, self.ctx)
 
+    def modwt_fwd_ld(self, x, c, n, J, w):
+        """forwardMODWT of x[:n] into the rows of c (row stride c.stride(0)),
+        columns [0, n); jwv_modwt_fwd_ld_f64_dev."""
+        T.modwt_forward_ld(x, c, n, J, w, self.ctx)
+
+    def modwt_inv_ld(self, c, col0, n, x, w):
+        """inverseMODWT of the columns [col0, col0 + n) of the rows of c into
+        x[:n]; jwv_modwt_inv_ld_f64_dev."""
+        T.modwt_inverse_ld(c, col0, n, x, w, self.ctx)
+
 
 def _world(group):
     return dist.get_world_size(group), dist.get_rank(group)
@@ -161,6 +171,75 @@ def _check_modwt(n_global, J, counts, H):
     if min(counts) < H:
         raise ValueError("sharded MODWT needs every slice >= the halo (%d < %d)"
                          % (min(counts), H))
+
+
+class ModwtShard:
+    """One rank's buffers of a sharded MODWT of one long signal
+    (MODWTTransform.java:256-375), laid out so that neither direction copies
+    a slice: H = modwt_halo(L, J).
+
+    * xe = [left halo (H) | x_local (n)]: the forward's extended periodic
+      signal; the ring exchange receives the halo straight into xe[:H].
+    * c: J+1 rows at stride ld = H + n + H.  The forward writes columns
+      [0, H + n); the kept coefficients are columns [H, H + n) (c_local);
+      the inverse's right halo -- the successor's first H kept columns --
+      lands in columns [H + n, 2H + n), and the inverse reads [H, 2H + n).
+    * xr: the inverse's n + H outputs; the first n are this rank's slice.
+    The wrap of each extended periodic transform reaches only the H outputs
+    that are dropped, and every kept output sums the same values in the same
+    order as the unsharded transform, so kept results are bit-identical."""
+
+    def __init__(self, n_global, w, J, device, group=None, dtype=torch.float64):
+        W, rank = _world(group)
+        counts = [shard_range(n_global, W, r)[1] for r in range(W)]
+        self.H = H = modwt_halo(w.mother_wavelength, J)
+        _check_modwt(n_global, J, counts, H)
+        self.W, self.rank, self.group = W, rank, group
+        self.n, self.J, self.w = counts[rank], J, w
+        self.start = shard_range(n_global, W, rank)[0]
+        n = self.n
+        self.ld = ld = H + n + H
+        self.xe = torch.empty(H + n, dtype=dtype, device=device)
+        self.x = self.xe[H:]
+        self.c = torch.empty((J + 1, ld), dtype=dtype, device=device)
+        self.xr = torch.empty(n + H, dtype=dtype, device=device)
+        self._send = torch.empty((J + 1, H), dtype=dtype, device=device)
+        self._recv = torch.empty((J + 1, H), dtype=dtype, device=device)
+
+    @property
+    def coeffs(self):
+        """This rank's [J+1][n] block of [W_1 .. W_J, V_J] (a strided view)."""
+        return self.c[:, self.H:self.H + self.n]
+
+    def exchange_forward(self):
+        """Left halo: my last H samples -> successor, predecessor's -> xe[:H]."""
+        if self.W > 1:
+            _ring_exchange(self.xe[self.n:self.n + self.H], self.xe[:self.H],
+                           (self.rank + 1) % self.W, (self.rank - 1) % self.W, self.group)
+        else:  # one rank: the periodic wrap of the whole signal
+            self.xe[:self.H].copy_(self.x[self.n - self.H:])
+
+    def exchange_inverse(self):
+        """Right halo: my first H kept columns -> predecessor, successor's ->
+        columns [H + n, 2H + n) (via a (J+1) x H staging pair)."""
+        H, n = self.H, self.n
+        self._send.copy_(self.c[:, H:2 * H])
+        if self.W > 1:
+            _ring_exchange(self._send, self._recv, (self.rank - 1) % self.W,
+                           (self.rank + 1) % self.W, self.group)
+            self.c[:, H + n:2 * H + n].copy_(self._recv)
+        else:
+            self.c[:, H + n:2 * H + n].copy_(self._send)
+
+    def forward(self, backend):
+        self.exchange_forward()
+        backend.modwt_fwd_ld(self.xe, self.c, self.H + self.n, self.J, self.w)
+        return self.coeffs
+
+    def inverse(self, backend):
+        self.exchange_inverse()
+        backend.modwt_inv_ld(self.c, self.H, self.n + self.H, self.xr, self.w)
+        return self.xr[:self.n]
 
 
 def modwt_forward(x_local, n_global, w, J, backend, group=None):

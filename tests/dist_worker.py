@@ -39,6 +39,13 @@ class OracleBackend:
     def modwt_inv(self, c, w):
         return torch.from_numpy(oracle.modwt_inverse(w, c.numpy()))
 
+    def modwt_fwd_ld(self, x, c, n, J, w):
+        c[:, :n] = torch.from_numpy(oracle.modwt_forward(w, x[:n].numpy(), J))
+
+    def modwt_inv_ld(self, c, col0, n, x, w):
+        x[:n] = torch.from_numpy(oracle.modwt_inverse(w, np.ascontiguousarray(
+            c[:, col0:col0 + n].numpy())))
+
 
 def same(a, b, what):
     a = a.detach().cpu().numpy() if torch.is_tensor(a) else a
@@ -107,6 +114,15 @@ def main():
         same(got, ref, "modwt fwd %s n=%d" % (wname, n))
         xr = D.modwt_inverse(cf, n, w, be)
         same(D.gather_rows(xr, n), oracle.modwt_inverse(w, ref), "modwt inv %s n=%d" % (wname, n))
+        # the same through the persistent strided buffers (no slice copies)
+        sh = D.ModwtShard(n, w, J, dev)
+        assert (sh.start, sh.n) == (s, c)
+        sh.x.copy_(put(full[s:s + c]))
+        for rep in range(2):  # reused buffers: the second call must not see the first's halos
+            cs = sh.forward(be)
+            same(D.gather_rows(cs.t().contiguous(), n).t(), ref, "shard fwd %s #%d" % (wname, rep))
+            same(D.gather_rows(sh.inverse(be).contiguous(), n), oracle.modwt_inverse(w, ref),
+                 "shard inv %s #%d" % (wname, rep))
 
     dist.barrier()
     dist.destroy_process_group()

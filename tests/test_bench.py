@@ -18,13 +18,18 @@ def _json_line(out):
     return json.loads(lines[-1])
 
 
-@pytest.mark.parametrize("gpus", [1, 2])
-def test_launcher_dry_run(gpus):
+@pytest.mark.parametrize("gpus,workload", [(1, "fwt1d"), (2, "fwt1d"), (2, "fwt2d"),
+                                           (2, "modwt"), (2, "wpt")])
+def test_launcher_dry_run(gpus, workload):
+    """The launcher at world 1 and 2 for every workload; at world 2 the
+    sharded configs 3 and 5 run their real exchanges (all-to-all transposes,
+    MODWT ring halos) over gloo around placeholder compute, and report the
+    exchange time apart."""
     env = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus),
-                        "--dry-run", "--steps", "3", "--warmup", "1"],
+                        "--dry-run", "--steps", "3", "--warmup", "1", "--workload", workload],
                        capture_output=True, text=True, timeout=240, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json_line(r.stdout)
@@ -33,6 +38,9 @@ def test_launcher_dry_run(gpus):
               "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
         assert k in d
     assert d["value"] > 0 and d["steps"] == 3
+    if gpus > 1 and workload in ("fwt2d", "modwt"):
+        assert d["scaling"] == "strong" and d["exchange_ms_per_step"] > 0
+        assert d["roundtrip_max_abs_err"] == 0.0  # placeholder compute: exact round trip
 
 
 def test_world_mismatch_is_explained():
