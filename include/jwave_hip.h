@@ -90,7 +90,8 @@ int jwv_ctx_set_math(jwv_ctx* ctx, int mode);
  * JWV_PLAN_FWD_TAIL: the forward's deep tiled pass and its resident pass in
  * one launch (the unit that completes an arrival counter runs the resident
  * levels; no wait).
- * Default: JWV_PLAN_REV_HEAD (env JWV_PLAN overrides the default flags). */
+ * Default: JWV_PLAN_REV_HEAD | JWV_PLAN_FWD_TAIL (env JWV_PLAN overrides the
+ * default flags). */
 #define JWV_PLAN_CHAIN_REV 1
 #define JWV_PLAN_CHAIN_FWD 2
 #define JWV_PLAN_REV_HEAD 4

@@ -29,6 +29,7 @@
 #include "../../include/jwave_hip.h"
 #include "jwv_launch.hpp"
 #include "jwv_stream.hpp"
+#include "jwv_modwt1.hpp"
 
 using jwv::AxisView;
 using jwv::Bank;
@@ -426,17 +427,24 @@ int fwt_res_cap(int C, int64_t outer) {
 
 // Cache policy of the full-length output stores of the forward (rev = 0) and
 // reverse (rev = 1) big passes (st2_pol: 0 plain, 1 sc1, 2 nt): env
-// JWV_STPOL_F / JWV_STPOL_R, else JWV_STPOL.
-int store_pol_dir(int rev) {
+// JWV_STPOL_F / JWV_STPOL_R, else JWV_STPOL.  Default: the reverse of one
+// 1-D signal (`final`: its output is the caller's result, not an
+// intermediate another pass reads next) stores non-temporal, so it does not
+// evict the coefficients a following reverse/forward pair streams from the
+// Infinity Cache (config 2 steady state over 3 alternating runs: 111.3-113.5
+// -> 109.0-111.3 us/step); forward outputs stay cacheable (nt on them: the
+// reverse that reads them next took 123 us/step).
+int store_pol_dir(int rev, bool final = false) {
   static const int p[2] = {[] {
                              const char* e = std::getenv("JWV_STPOL_F");
                              return e ? std::atoi(e) : Geo::store_pol();
                            }(),
                            [] {
                              const char* e = std::getenv("JWV_STPOL_R");
-                             return e ? std::atoi(e) : Geo::store_pol();
+                             return e ? std::atoi(e) : -1;
                            }()};
-  const int v = p[rev & 1];
+  int v = p[rev & 1];
+  if (rev && v < 0) v = final ? 2 : Geo::store_pol();
   return v < 0 || v > 2 ? 0 : v;
 }
 
@@ -607,7 +615,9 @@ void fwt_rev_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
     const AxisView ov = last ? a.dv : cview(hK, a.inner);
     jwv::TileArgs t{acur, acv, a.src, a.sv, out, ov, nullptr, {}, h1, K, a.outer, a.inner,
                     dma_view(acur, acv, C, a.inner) && dma_view(a.src, a.sv, C, a.inner),
-                    (last ? store_pol_dir(1) | (a.outer == 1 ? Geo::tile_desc(1) : 0) : 0) |
+                    (last ? store_pol_dir(1, a.outer == 1 && a.inner == 1) |
+                                (a.outer == 1 ? Geo::tile_desc(1) : 0)
+                          : 0) |
                         Geo::tile_walk()};
     { ProfScope ps_(c, last ? K_FWT_REV_TILE : K_FWT_REV_TILE_DEEP, 16.0 * a.outer * hK * a.inner);
     hipchk(jwv::launch_fwt_rev_tile(b, use_fma(c), C, t, c->stream), "fwt_rev_tile"); }
@@ -1065,6 +1075,16 @@ void check_modwt(int64_t n, int J) {
   }
 }
 
+// env JWV_MODWT_CT (default 1): the compile-time-geometry MODWT tiles
+// (modwt1_kernels.hpp) where they cover the case; 0 = the runtime tiles.
+bool modwt_ct() {
+  static const bool v = [] {
+    const char* e = std::getenv("JWV_MODWT_CT");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
 int64_t modwt_halo(int L, int j0, int j1) {
   return (int64_t)(L - 1) * ((int64_t(1) << j1) - (int64_t(1) << (j0 - 1)));
 }
@@ -1089,7 +1109,12 @@ void body_modwt_fwd(jwv_ctx* c, const Bank& b, const double* x, double* wv, int6
     {
       ProfScope ps_(c, tiled ? K_MODWT_FWD_TILE : K_MODWT_FWD_LEVEL,
                     8.0 * N * (1 + (j1 - j0 + 1) + 1));
-      hipchk(jwv::launch_modwt_fwd(m, use_fma(c), tiled, a, c->stream), "modwt_fwd");
+      hipError_t e = hipSuccess;
+      const bool ct = tiled && modwt_ct() &&
+                      (use_fma(c) ? jwv::fused::modwt_fwd1(m, a, c->stream, e)
+                                  : jwv::exact::modwt_fwd1(m, a, c->stream, e));
+      if (!ct) e = jwv::launch_modwt_fwd(m, use_fma(c), tiled, a, c->stream);
+      hipchk(e, "modwt_fwd");
     }
     vin = vout;
     pp ^= 1;
@@ -1115,7 +1140,12 @@ void body_modwt_inv(jwv_ctx* c, const Bank& b, const double* wv, double* x, int6
     {
       ProfScope ps_(c, tiled ? K_MODWT_INV_TILE : K_MODWT_INV_LEVEL,
                     8.0 * N * (1 + (j1 - j0 + 1) + 1));
-      hipchk(jwv::launch_modwt_inv(m, use_fma(c), tiled, a, c->stream), "modwt_inv");
+      hipError_t e = hipSuccess;
+      const bool ct = tiled && modwt_ct() &&
+                      (use_fma(c) ? jwv::fused::modwt_inv1(m, a, c->stream, e)
+                                  : jwv::exact::modwt_inv1(m, a, c->stream, e));
+      if (!ct) e = jwv::launch_modwt_inv(m, use_fma(c), tiled, a, c->stream);
+      hipchk(e, "modwt_inv");
     }
     vin = vout;
     pp ^= 1;
@@ -1233,7 +1263,7 @@ bool Geo::rev_pref() {
 #define JWV_MODE2(name, ...) \
   return fma ? fused::name(__VA_ARGS__) : exact::name(__VA_ARGS__)
 int ChainGeo::default_plan() {
-  static const int p = env_int("JWV_PLAN", JWV_PLAN_REV_HEAD) & 15;
+  static const int p = env_int("JWV_PLAN", JWV_PLAN_REV_HEAD | JWV_PLAN_FWD_TAIL) & 15;
   return p;
 }
 hipError_t launch_fwt_rev_head(const Bank& b, bool fma, const RevHeadArgs& a, hipStream_t s) {

@@ -33,13 +33,21 @@ __device__ __forceinline__ void fwd_pair_wrap(const FwdTaps<L>& tp, const double
 // lds[half, h).  Interior pairs (m >= Q-1) sum q descending from registers;
 // the array-head pairs (m < Q-1, lanes of wave 0) take rev_pair_head's order
 // through rev_pair_rot_t (inputs and taps tl from LDS, no register select).
+// rot (wave-uniform): every lane of the wave takes the rotated form (r = m
+// for head pairs, Q-1 = the interior order otherwise), so a wave holding
+// head pairs runs one path instead of both under divergence (the
+// latency-bound single-wave levels, and wave 0 of the block-wide ones).
 template <int L, bool FMA>
 __device__ __forceinline__ void rev_pair_wrap(const RevTaps<L>& tp, const double* tl,
                                               const double* lds, int half, int m, double& xe,
-                                              double& xo) {
+                                              double& xo, bool rot = false) {
   constexpr int Q = (L + 1) / 2;
   const int hm = half - 1;
-  if (m >= Q - 1) {
+  if (rot) {
+    rev_pair_rot_t<L, FMA>(tl, [=](int q) { return lds[(m - q) & hm]; },
+                           [=](int q) { return lds[half + ((m - q) & hm)]; },
+                           m < Q - 1 ? m : Q - 1, xe, xo);
+  } else if (m >= Q - 1) {
     double av[Q], dv[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
@@ -179,7 +187,7 @@ __device__ __forceinline__ void rev_res1_levels(double* lds, int h0, int nlev,
           }
           rev_small_c<L, FMA>(tp, av, dv, 1, hh, m, xe, xo);  // h < L: compile-time h
         } else {
-          rev_pair_wrap<L, FMA>(tp, tl, lds, half, m, xe, xo);
+          rev_pair_wrap<L, FMA>(tp, tl, lds, half, m, xe, xo, true);
         }
         wave_lds_sync();
         if (v) *reinterpret_cast<double2*>(lds + 2 * m) = make_double2(xe, xo);
@@ -196,7 +204,7 @@ __device__ __forceinline__ void rev_res1_levels(double* lds, int h0, int nlev,
     const int half = h >> 1;
     double xe[RM], xo[RM];
     auto slot = [&](int r) {
-      rev_pair_wrap<L, FMA>(tp, tl, lds, half, tid + r * NT, xe[r], xo[r]);
+      rev_pair_wrap<L, FMA>(tp, tl, lds, half, tid + r * NT, xe[r], xo[r], r == 0 && tid < 64);
     };
     const int R = half / NT;
     if (R <= 1) {

@@ -63,10 +63,11 @@ class Context:
 
     def set_plan(self, flags=None):
         """Pass plan for long single 1-D FWT signals (jwv_ctx_set_plan): a set
-        of {"rev_head", "chain_rev", "chain_fwd"}, empty = the multi-launch
-        plan, None = the default.  Results are bit-identical under every plan."""
+        of {"rev_head", "fwd_tail", "chain_rev", "chain_fwd"}, empty = the
+        multi-launch plan, None = the default.  Results are bit-identical under
+        every plan."""
         if flags is None:
-            flags = {"rev_head"}
+            flags = {"rev_head", "fwd_tail"}
         bits = {"chain_rev": L.JWV_PLAN_CHAIN_REV, "chain_fwd": L.JWV_PLAN_CHAIN_FWD,
                 "rev_head": L.JWV_PLAN_REV_HEAD, "fwd_tail": L.JWV_PLAN_FWD_TAIL}
         self._check(self._lib.jwv_ctx_set_plan(self.handle, sum(bits[f] for f in set(flags))))
