@@ -36,41 +36,73 @@ ModwtTaps<L> taps(const Bank& b) {
   return t;
 }
 
-// env JWV_MODWT_P2 (default 1): two adjacent outputs per lane (16-B LDS
-// reads); 0 = one output per lane
-bool p2() {
-  static const bool v = [] {
+// env JWV_MODWT_P2 (default 3): bit 0 forward, bit 1 inverse — two adjacent
+// outputs per lane (16-B LDS reads); a clear bit = one output per lane
+int p2_bits() {
+  static const int v = [] {
     const char* e = std::getenv("JWV_MODWT_P2");
-    return e ? std::atoi(e) != 0 : true;
+    return e ? std::atoi(e) : 3;
   }();
   return v;
 }
 
-template <int L, int J1, bool P2>
+template <int L, int J1, bool P2, int NT = kNT, int TF = kTF>
 hipError_t fwd_kp(const Bank& b, const ModwtArgs& a, hipStream_t s) {
-  auto k = modwt_fwd_tile1<L, kNT, kTF, 1, J1, kFMA, P2>;
-  const size_t lds = (size_t)ModFwd1Geo<L, kTF, 1, J1>::lds_doubles() * sizeof(double);
+  auto k = modwt_fwd_tile1<L, NT, TF, 1, J1, kFMA, P2>;
+  const size_t lds = (size_t)ModFwd1Geo<L, TF, 1, J1>::lds_doubles() * sizeof(double);
   if (hipError_t e = prep(k, lds)) return e;
-  const dim3 grid((unsigned)((a.N + kTF - 1) / kTF));
-  hipLaunchKernelGGL(k, grid, dim3(kNT), lds, s, a.src, a.wout, a.ldw, a.vout, a.N, taps<L>(b));
+  const dim3 grid((unsigned)((a.N + TF - 1) / TF));
+  hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.wout, a.ldw, a.vout, a.N, taps<L>(b));
   return hipGetLastError();
 }
-template <int L, int J1, bool P2>
+// tile geometry of the full-depth (J1 = 8) launches: env JWV_MODWT_GF (forward)
+// / JWV_MODWT_GI (inverse) = 0 default, 1.. the alternatives below
+int geo_env(const char* name) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : 0;
+}
+int geo_f() { static const int v = geo_env("JWV_MODWT_GF"); return v; }
+int geo_i() { static const int v = geo_env("JWV_MODWT_GI"); return v; }
+template <int L, int J1, bool P2, int NT = kNT, int TI = kTI>
 hipError_t inv_kp(const Bank& b, const ModwtArgs& a, hipStream_t s) {
-  auto k = modwt_inv_tile1<L, kNT, kTI, 1, J1, kFMA, P2>;
-  const size_t lds = (size_t)ModInv1Geo<L, kTI, 1, J1>::lds_doubles() * sizeof(double);
+  auto k = modwt_inv_tile1<L, NT, TI, 1, J1, kFMA, P2>;
+  const size_t lds = (size_t)ModInv1Geo<L, TI, 1, J1>::lds_doubles() * sizeof(double);
   if (hipError_t e = prep(k, lds)) return e;
-  const dim3 grid((unsigned)((a.N + kTI - 1) / kTI));
-  hipLaunchKernelGGL(k, grid, dim3(kNT), lds, s, a.src, a.coef, a.ldw, a.vout, a.N, taps<L>(b));
+  const dim3 grid((unsigned)((a.N + TI - 1) / TI));
+  hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.coef, a.ldw, a.vout, a.N, taps<L>(b));
   return hipGetLastError();
 }
+// Full-depth forward (J1 = 8, config 5): 1024 x 8192 tiles (half the halo
+// recompute of 4096-sample tiles; 16 waves per CU either way): 186-188 ->
+// 173-176 us per launch (two runs, one box); 512 x 8192 (200 us) and
+// 256 x 4096 (214 us) measured slower.  JWV_MODWT_GF selects the others.
 template <int L, int J1>
 hipError_t fwd_k(const Bank& b, const ModwtArgs& a, hipStream_t s) {
-  return p2() ? fwd_kp<L, J1, true>(b, a, s) : fwd_kp<L, J1, false>(b, a, s);
+  if constexpr (J1 == 8) {
+    switch (geo_f()) {
+      case 1: return fwd_kp<L, J1, true, 512, 8192>(b, a, s);
+      case 3: return fwd_kp<L, J1, true, 256, 4096>(b, a, s);
+      case 4: return fwd_kp<L, J1, true, 512, 4096>(b, a, s);
+      case 5: return fwd_kp<L, J1, true, 1024, 16384>(b, a, s);
+      default:
+        if (p2_bits() & 1) return fwd_kp<L, J1, true, 1024, 8192>(b, a, s);
+        break;
+    }
+  }
+  return (p2_bits() & 1) ? fwd_kp<L, J1, true>(b, a, s) : fwd_kp<L, J1, false>(b, a, s);
 }
 template <int L, int J1>
 hipError_t inv_k(const Bank& b, const ModwtArgs& a, hipStream_t s) {
-  return p2() ? inv_kp<L, J1, true>(b, a, s) : inv_kp<L, J1, false>(b, a, s);
+  if constexpr (J1 == 8) {
+    switch (geo_i()) {
+      case 1: return inv_kp<L, J1, true, 512, 1024>(b, a, s);
+      case 2: return inv_kp<L, J1, true, 256, 1024>(b, a, s);
+      case 3: return inv_kp<L, J1, true, 1024, 4096>(b, a, s);
+      case 4: return inv_kp<L, J1, true, 256, 2048>(b, a, s);
+      default: break;
+    }
+  }
+  return (p2_bits() & 2) ? inv_kp<L, J1, true>(b, a, s) : inv_kp<L, J1, false>(b, a, s);
 }
 template <int L, bool FWD>
 hipError_t go(const Bank& b, const ModwtArgs& a, hipStream_t s) {

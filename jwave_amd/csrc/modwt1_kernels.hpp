@@ -39,25 +39,28 @@ struct ModFwd1Geo {
   static constexpr int lds_doubles() { return W + 8; }  // + pad and one pair past the end
 };
 
-// P2: a lane computes the two adjacent outputs (e, e+1), e even (level j
-// starts at e0 rounded down to even: the extra output below e0 reads below
-// the level's valid input and is never read or stored), so every tap pair
-// (e - l*st, e + 1 - l*st) is one 16-B LDS read (st even; st = 1 reads the
-// 10-value run e-8 .. e+1) at a 16-B lane stride; the window sits at
-// lds + kPad so those reads stay inside the allocation.
+// P2: a lane computes two adjacent outputs (e, e+1) with e of the parity of
+// e0(j) (= the parity of S for every level: Sn(j) is even), so the pairs
+// tile each level's outputs exactly; the window sits at lds + kPad with kPad
+// + e0 even, so every tap pair (e - l*st, e + 1 - l*st) is one 16-B LDS read
+// (st = 1: the 10-value run e-8 .. e+1) at a 16-B lane stride, and the W
+// pair (t0 - S + e even) is one 16-B store when the rows are 16-B aligned.
 template <int L, int NT, int T, int J0, int J1, bool FMA, int j, bool P2>
 struct ModFwd1Level {
-  static constexpr int kPad = 2;
+  static constexpr int kPad = (ModFwd1Geo<L, T, J0, J1>::S & 1) ? 1 : 2;
   __device__ __forceinline__ static void run_p2(const ModwtTaps<L>& tp, double* lds,
                                                 double* __restrict__ wout, int64_t ldw,
                                                 int64_t t0, int64_t N) {
     using G = ModFwd1Geo<L, T, J0, J1>;
     constexpr int st = 1 << (j - 1);
-    constexpr int e0 = G::e0(j) & ~1, nout = G::nout(j) + (G::e0(j) & 1);
-    constexpr int NP = (nout + 1) / 2;
+    constexpr int e0 = G::e0(j), nout = G::nout(j);
+    static_assert(((kPad + e0) & 1) == 0 && (nout & 1) == 0, "pairs must tile the outputs");
+    constexpr int NP = nout / 2;
     constexpr int R = (NP + NT - 1) / NT;
     const int tid = opaque_tid();
     double* __restrict__ wrow = wout + (int64_t)(j - 1) * ldw + (t0 - G::S);
+    // 16-B W stores: row base (j-1)*ldw + t0 - S + e is even for these e
+    const bool w16 = (((uintptr_t)wrow + 8 * e0) & 15) == 0;
     double2 vv[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -99,14 +102,19 @@ struct ModFwd1Level {
       pin2(sw0, sv0);
       pin2(sw1, sv1);
       vv[r] = make_double2(sv0, sv1);
-      const int ee = e0 + 2 * k;
-      const bool v = full || k < NP;
-      if (v && !(e0 + 2 * ((r + 1) * NT) - 1 < G::S)) {
-        if (ee >= G::S && t0 + (ee - G::S) < N) wrow[ee] = sw0;
-        if (ee + 1 >= G::S && ee + 1 < G::S + T && t0 + (ee + 1 - G::S) < N) wrow[ee + 1] = sw1;
+      const int ee = e0 + 2 * k;  // S has e0's parity: a pair is all halo or all own
+      if ((full || k < NP) && e0 + 2 * (r + 1) * NT > G::S && ee >= G::S) {
+        const int64_t g = t0 + (ee - G::S);
+        if (w16 && g + 1 < N) {
+          *reinterpret_cast<double2*>(wrow + ee) = make_double2(sw0, sw1);
+        } else {
+          if (g < N) wrow[ee] = sw0;
+          if (g + 1 < N) wrow[ee + 1] = sw1;
+        }
       }
       if constexpr (JWV_MOD1_FENCE > 0)
-        if ((r + 1) % JWV_MOD1_FENCE == 0) asm volatile("" : "+v"(vv[r].x), "+v"(vv[r].y) :: "memory");
+        if ((r + 1) % JWV_MOD1_FENCE == 0)
+          asm volatile("" : "+v"(vv[r].x), "+v"(vv[r].y) :: "memory");
     }
     lds_barrier();
 #pragma unroll
