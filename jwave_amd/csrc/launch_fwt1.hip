@@ -1,12 +1,12 @@
-// launch_fwt1.hip — dispatch of the C = 1 compile-time-geometry FWT tile
-// kernels (fwt1_kernels.hpp) for one math mode (compiled twice, like
-// launch_fwt_wpt.hip).  Used for contiguous, 16-B aligned signals with a
+// launch_fwt1.hip — dispatch of the C = 1 compile-time-geometry FWT kernels
+// (tiles fwt1_kernels.hpp, resident fwt1_res.hpp, wave-per-row fwt1_row.hpp)
+// for one math mode (compiled twice, like launch_fwt_wpt.hip; the WPT and
+// column-slab tiles live in launch_wpt1.hip / launch_fwt8.hip).  Used for contiguous, 16-B aligned signals with a
 // compiled-in tap count; every other case keeps the generic tile kernels.
 #include "fwt1_kernels.hpp"
 #include <cstdlib>
 #include "fwt1_res.hpp"
-#include "fwt8_kernels.hpp"
-#include "wpt1_kernels.hpp"
+#include "fwt1_row.hpp"
 #include "jwv_launch.hpp"
 
 #ifndef JWV_FMA
@@ -140,112 +140,6 @@ hipError_t rev_res1_l(const Bank& b, const ResArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// ---- WPT
-constexpr int kWptT = Geo::kWpt1T;
-template <int L, int K>
-hipError_t wfwd1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
-  auto k = wpt_fwd_tile1<L, 256, kWptT, K, kFMA>;
-  const size_t lds = (size_t)Wpt1FwdGeo<L, kWptT, K>::lds_doubles() * sizeof(double);
-  if (hipError_t e = prep1(k, lds)) return e;
-  FwdTaps<L> tp;
-  for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
-  const dim3 grid((unsigned)(a.nouter * (a.h / kWptT)));
-  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a.src, a.sv, a.dst, a.dv, a.h, tp);
-  return hipGetLastError();
-}
-template <int L, int K>
-hipError_t wrev1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
-  auto k = wpt_rev_tile1<L, 256, kWptT, K, kFMA>;
-  const size_t lds = (size_t)Wpt1RevGeo<L, kWptT, K>::lds_doubles() * sizeof(double);
-  if (hipError_t e = prep1(k, lds)) return e;
-  RevTaps<L> tp;
-  for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
-  const dim3 grid((unsigned)(a.nouter * (a.h / kWptT)));
-  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a.src, a.sv, a.dst, a.dv, a.h, tp);
-  return hipGetLastError();
-}
-// 8192-sample forward WPT tiles, 512 threads: half the halo recompute of the
-// 4096 tile (14.7% -> 7.4% extra pairs) at the same waves per CU.  Config 4
-// forward 2597 -> 2468 us; the reverse (halo ~7% at 4096) measured no gain
-// and keeps 4096.  env JWV_WPT8K=0: 4096 for both.
-template <int L, bool FWD>
-hipError_t wpt8k(const Bank& b, const TileArgs& a, hipStream_t s) {
-  constexpr int TT = 8192, K = 6;
-  const dim3 grid((unsigned)(a.nouter * (a.h / TT)));
-  if constexpr (FWD) {
-    auto k = wpt_fwd_tile1<L, 512, TT, K, kFMA>;
-    const size_t lds = (size_t)Wpt1FwdGeo<L, TT, K>::lds_doubles() * sizeof(double);
-    if (hipError_t e = prep1(k, lds)) return e;
-    FwdTaps<L> tp;
-    for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
-    hipLaunchKernelGGL(k, grid, dim3(512), lds, s, a.src, a.sv, a.dst, a.dv, a.h, tp);
-  } else {
-    auto k = wpt_rev_tile1<L, 512, TT, K, kFMA>;
-    const size_t lds = (size_t)Wpt1RevGeo<L, TT, K>::lds_doubles() * sizeof(double);
-    if (hipError_t e = prep1(k, lds)) return e;
-    RevTaps<L> tp;
-    for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
-    hipLaunchKernelGGL(k, grid, dim3(512), lds, s, a.src, a.sv, a.dst, a.dv, a.h, tp);
-  }
-  return hipGetLastError();
-}
-bool wpt_8k() {
-  static const bool v = [] {
-    const char* e = std::getenv("JWV_WPT8K");
-    return e ? std::atoi(e) != 0 : true;
-  }();
-  return v;
-}
-template <int L>
-hipError_t wpt1_l(const Bank& b, const TileArgs& a, hipStream_t s, bool fwd) {
-  if (fwd && a.K == 6 && a.h % 8192 == 0 && wpt_8k()) return wpt8k<L, true>(b, a, s);
-  switch (a.K) {
-    case 1: return fwd ? wfwd1_k<L, 1>(b, a, s) : wrev1_k<L, 1>(b, a, s);
-    case 2: return fwd ? wfwd1_k<L, 2>(b, a, s) : wrev1_k<L, 2>(b, a, s);
-    case 3: return fwd ? wfwd1_k<L, 3>(b, a, s) : wrev1_k<L, 3>(b, a, s);
-    case 4: return fwd ? wfwd1_k<L, 4>(b, a, s) : wrev1_k<L, 4>(b, a, s);
-    case 5: return fwd ? wfwd1_k<L, 5>(b, a, s) : wrev1_k<L, 5>(b, a, s);
-    default: return fwd ? wfwd1_k<L, 6>(b, a, s) : wrev1_k<L, 6>(b, a, s);
-  }
-}
-
-// ---- C = 8 column slabs (fwt8_kernels.hpp); tile rows = the generic C = 8
-// tile the planner sizes grids and workspaces for
-constexpr int kT8 = Geo::kFwtT8;
-template <int L, int K>
-hipError_t fwd8_k(const Bank& b, const TileArgs& a, hipStream_t s) {
-  auto k = fwt_fwd_tile8<L, 256, kT8, K, kFMA>;
-  const size_t lds = (size_t)Fwd8Geo<L, kT8, K>::lds_doubles() * sizeof(double);
-  if (hipError_t e = prep1(k, lds)) return e;
-  FwdTaps<L> tp;
-  for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
-  const dim3 grid((unsigned)(a.nouter * (a.inner / 8) * (a.h / kT8)));
-  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a.src, a.sv, a.dst, a.dv, a.adst, a.av, a.h,
-                     a.inner, tp, Geo::slab_order());
-  return hipGetLastError();
-}
-template <int L, int K>
-hipError_t rev8_k(const Bank& b, const TileArgs& a, hipStream_t s) {
-  auto k = fwt_rev_tile8<L, 256, kT8, K, kFMA>;
-  const size_t lds = (size_t)Rev8Geo<L, kT8, K>::lds_doubles() * sizeof(double);
-  if (hipError_t e = prep1(k, lds)) return e;
-  RevTaps<L> tp;
-  for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
-  const int hK = a.h << (a.K - 1);
-  const dim3 grid((unsigned)(a.nouter * (a.inner / 8) * (hK / kT8)));
-  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a.src, a.sv, a.coef, a.cv, a.dst, a.dv, hK,
-                     a.inner, tp, Geo::slab_order());
-  return hipGetLastError();
-}
-template <int L>
-hipError_t tile8_l(const Bank& b, const TileArgs& a, hipStream_t s, bool fwd) {
-  switch (a.K) {
-    case 1: return fwd ? fwd8_k<L, 1>(b, a, s) : rev8_k<L, 1>(b, a, s);
-    case 2: return fwd ? fwd8_k<L, 2>(b, a, s) : rev8_k<L, 2>(b, a, s);
-    default: return fwd ? fwd8_k<L, 3>(b, a, s) : rev8_k<L, 3>(b, a, s);
-  }
-}
-
 bool plain(const AxisView& v) { return v.pk == 1 && v.s_len == 1; }
 // packet views: stride-1 samples, even strides (16-B aligned packet rows)
 bool pk_ok(const AxisView& v) {
@@ -284,13 +178,51 @@ bool res1_rows() {
   }();
   return v;
 }
+// Batches of >= 64 rows up to kSmallH samples (the row passes' resident
+// tails, config 3): one wave per row (fwt1_row.hpp), env JWV_SMALL1=0: the
+// block-per-row kernels above.  Config 3 tails (8192 rows, one box):
+// forward 45.8 -> 40.1 us, reverse 79.0 -> 73.9 us.
+bool small1() {
+  static const bool v = [] {
+    const char* e = std::getenv("JWV_SMALL1");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+template <int L>
+hipError_t fwd_small1_l(const Bank& b, const ResArgs& a, hipStream_t s) {
+  FwdTaps<L> tp;
+  for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
+  auto k = fwt_fwd_small1<L, kFMA>;
+  hipLaunchKernelGGL(k, dim3((unsigned)((a.nouter + kSmallRows - 1) / kSmallRows)),
+                     dim3(64 * kSmallRows), 0, s, a.src, a.sv.s_outer, a.dst, a.dv.s_outer, a.n,
+                     a.nlev, a.nouter, tp);
+  return hipGetLastError();
+}
+template <int L>
+hipError_t rev_small1_l(const Bank& b, const ResArgs& a, hipStream_t s) {
+  RevTaps<L> tp;
+  for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
+  auto k = fwt_rev_small1<L, kFMA>;
+  hipLaunchKernelGGL(k, dim3((unsigned)((a.nouter + kSmallRows - 1) / kSmallRows)),
+                     dim3(64 * kSmallRows), 0, s, a.src, a.sv.s_outer, a.dst, a.dv.s_outer, a.n,
+                     a.nlev, a.nouter, tp);
+  return hipGetLastError();
+}
+// rows the wave-per-row kernels take (level input n / reverse top htop)
+bool small1_case(const ResArgs& a, int64_t htop) {
+  return small1() && a.nouter >= 64 && htop <= kSmallH && a.nlev >= 1;
+}
+
 template <int L>
 hipError_t fwd_res1_pick(const Bank& b, const ResArgs& a, hipStream_t s) {
+  if (small1_case(a, a.n)) return fwd_small1_l<L>(b, a, s);
   if (a.nouter >= 64) return fwd_res1_l<L, 256, kRowCap>(b, a, s);
   return fwd_res1_l<L, 1024, kCap>(b, a, s);
 }
 template <int L>
 hipError_t rev_res1_pick(const Bank& b, const ResArgs& a, hipStream_t s) {
+  if (a.nlev > 0 && small1_case(a, (int64_t)a.n << (a.nlev - 1))) return rev_small1_l<L>(b, a, s);
   if (a.nouter >= 64) return rev_res1_l<L, 256, kRowCap>(b, a, s);
   return rev_res1_l<L, 1024, kCap>(b, a, s);
 }
@@ -318,34 +250,6 @@ bool fwt_rev_res1(const Bank& b, const ResArgs& a, hipStream_t s, hipError_t& er
     case 4: err = rev_res1_pick<4>(b, a, s); return true;
     case 8: err = rev_res1_pick<8>(b, a, s); return true;
     case 16: err = rev_res1_pick<16>(b, a, s); return true;
-    default: return false;
-  }
-}
-bool wpt_tile1(const Bank& b, const TileArgs& a, hipStream_t s, bool fwd, hipError_t& err) {
-  if (!Geo::fwt1() || !a.dma || a.inner != 1 || (!fwd && b.scale != 1.0)) return false;
-  if (!pk_ok(a.sv) || !pk_ok(a.dv) || a.K < 1 || a.K > Geo::kWpt1KMax) return false;
-  if (((uintptr_t)a.dst & 15) || ((uintptr_t)a.src & 15) || a.h < kWptT || a.h % kWptT) return false;
-  switch (b.L) {
-    case 2: err = wpt1_l<2>(b, a, s, fwd); return true;
-    case 4: err = wpt1_l<4>(b, a, s, fwd); return true;
-    case 8: err = wpt1_l<8>(b, a, s, fwd); return true;
-    case 16: err = wpt1_l<16>(b, a, s, fwd); return true;
-    default: return false;
-  }
-}
-// C = 8 slabs: every row segment 16-B aligned (a.dma), whole slabs, a
-// compiled-in tap count, at most Geo::kFwtK8 levels (the generic bound).
-bool fwt_tile8(const Bank& b, const TileArgs& a, hipStream_t s, bool fwd, hipError_t& err) {
-  if (!Geo::fwt8() || !a.dma || a.inner % 8 || a.K < 1 || a.K > 3 || a.K > Geo::kFwtK8)
-    return false;
-  if (!fwd && b.scale != 1.0) return false;
-  const int64_t hT = fwd ? (int64_t)a.h : ((int64_t)a.h << (a.K - 1));
-  if (hT < kT8 || hT % kT8) return false;
-  switch (b.L) {
-    case 2: err = tile8_l<2>(b, a, s, fwd); return true;
-    case 4: err = tile8_l<4>(b, a, s, fwd); return true;
-    case 8: err = tile8_l<8>(b, a, s, fwd); return true;
-    case 16: err = tile8_l<16>(b, a, s, fwd); return true;
     default: return false;
   }
 }

@@ -1,0 +1,84 @@
+// launch_fwt8.hip — dispatch of the C = 8 column-slab tiles
+// (fwt8_kernels.hpp) for one math mode (compiled twice).
+#include "fwt8_kernels.hpp"
+#include <cstdlib>
+#include "jwv_launch.hpp"
+
+#ifndef JWV_FMA
+#error "JWV_FMA must be 0 or 1"
+#endif
+#if JWV_FMA
+#define JWV_NS fused
+#else
+#define JWV_NS exact
+#endif
+
+namespace jwv {
+namespace {
+constexpr bool kFMA = JWV_FMA != 0;
+
+template <typename Kern>
+hipError_t prep1(Kern kernel, size_t lds) {
+  if (lds > 65536)
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  return hipSuccess;
+}
+// ---- C = 8 column slabs (fwt8_kernels.hpp); tile rows = the generic C = 8
+// tile the planner sizes grids and workspaces for
+constexpr int kT8 = Geo::kFwtT8;
+template <int L, int K>
+hipError_t fwd8_k(const Bank& b, const TileArgs& a, hipStream_t s) {
+  auto k = fwt_fwd_tile8<L, 256, kT8, K, kFMA>;
+  const size_t lds = (size_t)Fwd8Geo<L, kT8, K>::lds_doubles() * sizeof(double);
+  if (hipError_t e = prep1(k, lds)) return e;
+  FwdTaps<L> tp;
+  for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
+  const dim3 grid((unsigned)(a.nouter * (a.inner / 8) * (a.h / kT8)));
+  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a.src, a.sv, a.dst, a.dv, a.adst, a.av, a.h,
+                     a.inner, tp, Geo::slab_order());
+  return hipGetLastError();
+}
+template <int L, int K>
+hipError_t rev8_k(const Bank& b, const TileArgs& a, hipStream_t s) {
+  auto k = fwt_rev_tile8<L, 256, kT8, K, kFMA>;
+  const size_t lds = (size_t)Rev8Geo<L, kT8, K>::lds_doubles() * sizeof(double);
+  if (hipError_t e = prep1(k, lds)) return e;
+  RevTaps<L> tp;
+  for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
+  const int hK = a.h << (a.K - 1);
+  const dim3 grid((unsigned)(a.nouter * (a.inner / 8) * (hK / kT8)));
+  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a.src, a.sv, a.coef, a.cv, a.dst, a.dv, hK,
+                     a.inner, tp, Geo::slab_order());
+  return hipGetLastError();
+}
+template <int L>
+hipError_t tile8_l(const Bank& b, const TileArgs& a, hipStream_t s, bool fwd) {
+  switch (a.K) {
+    case 1: return fwd ? fwd8_k<L, 1>(b, a, s) : rev8_k<L, 1>(b, a, s);
+    case 2: return fwd ? fwd8_k<L, 2>(b, a, s) : rev8_k<L, 2>(b, a, s);
+    default: return fwd ? fwd8_k<L, 3>(b, a, s) : rev8_k<L, 3>(b, a, s);
+  }
+}
+
+}  // namespace
+
+namespace JWV_NS {
+// C = 8 slabs: every row segment 16-B aligned (a.dma), whole slabs, a
+// compiled-in tap count, at most Geo::kFwtK8 levels (the generic bound).
+bool fwt_tile8(const Bank& b, const TileArgs& a, hipStream_t s, bool fwd, hipError_t& err) {
+  if (!Geo::fwt8() || !a.dma || a.inner % 8 || a.K < 1 || a.K > 3 || a.K > Geo::kFwtK8)
+    return false;
+  if (!fwd && b.scale != 1.0) return false;
+  const int64_t hT = fwd ? (int64_t)a.h : ((int64_t)a.h << (a.K - 1));
+  if (hT < kT8 || hT % kT8) return false;
+  switch (b.L) {
+    case 2: err = tile8_l<2>(b, a, s, fwd); return true;
+    case 4: err = tile8_l<4>(b, a, s, fwd); return true;
+    case 8: err = tile8_l<8>(b, a, s, fwd); return true;
+    case 16: err = tile8_l<16>(b, a, s, fwd); return true;
+    default: return false;
+  }
+}
+}  // namespace JWV_NS
+}  // namespace jwv

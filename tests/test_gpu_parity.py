@@ -307,7 +307,7 @@ def test_fwt2d_rowcap(ctx, ctx_fma, wname, shape):
             assert_close(T.transform_2d(yr, w, lm, ln, False, ctx_fma), xr, "2d rev fma")
 
 
-@pytest.mark.parametrize("wname", ["Haar1", "Daubechies4", "Daubechies8", "Symlet8"])
+@pytest.mark.parametrize("wname", ["Haar1", "Daubechies2", "Daubechies4", "Daubechies8", "Symlet8"])
 def test_fwt_batch_rowcap(ctx, wname):
     """Batched 1-D FWT, 64 signals x 8192 (>= 64 rows, > 2048 samples: the
     row-cap branch), and 100 x 4096 (not a multiple of 8 rows), all levels

@@ -13,7 +13,7 @@ for wl in fwt2d wpt modwt; do
   cat $O/bench_$wl.json
 done
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/prof.log 2>&1 || { echo ROCPROF FAILED; tail -20 $O/prof.log; exit 4; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --warmup-seconds 0 > $O/prof.log 2>&1 || { echo ROCPROF FAILED; tail -20 $O/prof.log; exit 4; }
 python tools/trace_summary.py $O/prof
 bash tools/gpu_pmc.sh $TAG/pmc exact fwt1d fwt2d wpt modwt || exit 5
 

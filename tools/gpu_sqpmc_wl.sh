@@ -11,6 +11,6 @@ P3="SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INST_CY
 i=0
 for P in "$P1" "$P2" "$P3"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d $O/p$i -o run -- python bench.py --workload $WL --math $M --steps 2 --warmup 1 --no-cpu-baseline > $O/p$i.log 2>&1 || { echo "PMC $i FAILED"; tail $O/p$i.log; exit $i; }
+  timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d $O/p$i -o run -- python bench.py --workload $WL --math $M --steps 2 --warmup 1 --no-cpu-baseline --warmup-seconds 0 > $O/p$i.log 2>&1 || { echo "PMC $i FAILED"; tail $O/p$i.log; exit $i; }
 done
 python tools/pmc_summary.py $O
