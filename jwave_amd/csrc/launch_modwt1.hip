@@ -46,13 +46,47 @@ int p2_bits() {
   return v;
 }
 
-template <int L, int J1, bool P2, int NT = kNT, int TF = kTF>
+template <int L, int J1, bool P2, int NT = kNT, int TF = kTF, int M = 1>
 hipError_t fwd_kp(const Bank& b, const ModwtArgs& a, hipStream_t s) {
-  auto k = modwt_fwd_tile1<L, NT, TF, 1, J1, kFMA, P2>;
-  const size_t lds = (size_t)ModFwd1Geo<L, TF, 1, J1>::lds_doubles() * sizeof(double);
+  auto k = modwt_fwd_tile1<L, NT, TF, 1, J1, kFMA, P2, M>;
+  const size_t lds = (size_t)ModFwd1Geo<L, TF, 1, J1>::lds_doubles(M) * sizeof(double);
   if (hipError_t e = prep(k, lds)) return e;
   const dim3 grid((unsigned)((a.N + TF - 1) / TF));
   hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.wout, a.ldw, a.vout, a.N, taps<L>(b));
+  return hipGetLastError();
+}
+// Persistent forward (modwt_fwd_tile1p): blocks per CU x CUs, rounded to a
+// multiple of 8 (XCDs); env JWV_MODWT_PF = 0 keeps the one-tile-per-block grid
+int pf_env() {
+  static const int v = [] {
+    const char* e = std::getenv("JWV_MODWT_PF");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v;
+}
+int cu_count() {
+  static const int v = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 8)
+      n = 256;
+    return n;
+  }();
+  return v;
+}
+template <int L, int J1, int NT, int TF, int M = 1>
+hipError_t fwd_kpp(const Bank& b, const ModwtArgs& a, hipStream_t s) {
+  auto k = modwt_fwd_tile1p<L, NT, TF, 1, J1, kFMA, true, M>;
+  const size_t lds = (size_t)ModFwd1Geo<L, TF, 1, J1>::lds_doubles(M) * sizeof(double);
+  if (hipError_t e = prep(k, lds)) return e;
+  const int64_t ntile = (a.N + TF - 1) / TF;
+  const int per_cu = lds > 81920 ? 1 : 2;
+  int64_t nb = (int64_t)(cu_count() / 8) * per_cu;  // blocks per XCD
+  const int64_t need = (ntile + 7) / 8;            // tiles per XCD chunk
+  if (nb > need) nb = need;
+  if (nb < 1) nb = 1;
+  hipLaunchKernelGGL(k, dim3((unsigned)(8 * nb)), dim3(NT), lds, s, a.src, a.wout, a.ldw, a.vout,
+                     a.N, taps<L>(b));
   return hipGetLastError();
 }
 // tile geometry of the full-depth (J1 = 8) launches: env JWV_MODWT_GF (forward)
@@ -62,11 +96,25 @@ int geo_env(const char* name) {
   return e ? std::atoi(e) : 0;
 }
 int geo_f() { static const int v = geo_env("JWV_MODWT_GF"); return v; }
+// Run form (ModRun) of the full-depth launches: env JWV_MODWT_RUN (inverse) /
+// JWV_MODWT_RUNF (forward) = m + 100*jr, m pairs per lane on levels j >= jr
+// (3, 303, 503; 1 = the two-output P2 form on every level)
+int run_env(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+// inverse: 303 (r03, one box, two rounds: 235.3 / 236.8 us against 250.0 /
+// 252.1 for the P2 form, 243.5 / 239.7 for 3, 239.1 / 237.9 for 503)
+int run_m() { static const int v = run_env("JWV_MODWT_RUN", 303); return v; }
+// forward (env JWV_MODWT_RUNF): 1, the P2 form (r03: 176.3 / 174.4 us against
+// 207.9 / 209.4 for 3, 203.6 / 203.0 for 303, 206.0 / 205.1 for 503 — the run
+// form's W stores leave the wave as H-slot runs M*H slots apart)
+int run_f() { static const int v = run_env("JWV_MODWT_RUNF", 1); return v; }
 int geo_i() { static const int v = geo_env("JWV_MODWT_GI"); return v; }
-template <int L, int J1, bool P2, int NT = kNT, int TI = kTI>
+template <int L, int J1, bool P2, int NT = kNT, int TI = kTI, int M = 1>
 hipError_t inv_kp(const Bank& b, const ModwtArgs& a, hipStream_t s) {
-  auto k = modwt_inv_tile1<L, NT, TI, 1, J1, kFMA, P2>;
-  const size_t lds = (size_t)ModInv1Geo<L, TI, 1, J1>::lds_doubles() * sizeof(double);
+  auto k = modwt_inv_tile1<L, NT, TI, 1, J1, kFMA, P2, M>;
+  const size_t lds = (size_t)ModInv1Geo<L, TI, 1, J1>::lds_doubles(M) * sizeof(double);
   if (hipError_t e = prep(k, lds)) return e;
   const dim3 grid((unsigned)((a.N + TI - 1) / TI));
   hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.coef, a.ldw, a.vout, a.N, taps<L>(b));
@@ -85,7 +133,16 @@ hipError_t fwd_k(const Bank& b, const ModwtArgs& a, hipStream_t s) {
       case 4: return fwd_kp<L, J1, true, 512, 4096>(b, a, s);
       case 5: return fwd_kp<L, J1, true, 1024, 16384>(b, a, s);
       default:
-        if (p2_bits() & 1) return fwd_kp<L, J1, true, 1024, 8192>(b, a, s);
+        if (p2_bits() & 1) {
+          if (pf_env() == 1 && run_f() == 1) return fwd_kpp<L, J1, 1024, 8192>(b, a, s);
+          switch (run_f()) {
+            case 3: return fwd_kp<L, J1, true, 1024, 8192, 3>(b, a, s);
+            case 303: return fwd_kp<L, J1, true, 1024, 8192, 303>(b, a, s);
+            case 503: return fwd_kp<L, J1, true, 1024, 8192, 503>(b, a, s);
+            default: break;
+          }
+          return fwd_kp<L, J1, true, 1024, 8192>(b, a, s);
+        }
         break;
     }
   }
@@ -99,7 +156,16 @@ hipError_t inv_k(const Bank& b, const ModwtArgs& a, hipStream_t s) {
       case 2: return inv_kp<L, J1, true, 256, 1024>(b, a, s);
       case 3: return inv_kp<L, J1, true, 1024, 4096>(b, a, s);
       case 4: return inv_kp<L, J1, true, 256, 2048>(b, a, s);
-      default: break;
+      default:
+        if (p2_bits() & 2) {
+          switch (run_m()) {
+            case 3: return inv_kp<L, J1, true, kNT, kTI, 3>(b, a, s);
+            case 303: return inv_kp<L, J1, true, kNT, kTI, 303>(b, a, s);
+            case 503: return inv_kp<L, J1, true, kNT, kTI, 503>(b, a, s);
+            default: break;
+          }
+        }
+        break;
     }
   }
   return (p2_bits() & 2) ? inv_kp<L, J1, true>(b, a, s) : inv_kp<L, J1, false>(b, a, s);

@@ -25,6 +25,54 @@ namespace jwv {
 #define JWV_MOD1_FENCE 2
 #endif
 
+// Buffer-resource access for tiles that do not wrap: the block-uniform base
+// lives in SGPRs, a lane adds one 32-bit offset, slot offsets are scalar, so a
+// load or store costs no per-access 64-bit address VALU.
+__device__ __forceinline__ auto mod_rsrc(const double* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), 0, 0x7ffffff0, 0x00020000);
+}
+// lds[e] = src[e], e < W (no wrap), loads all in flight before the LDS writes
+template <int NT, int MAXP>
+__device__ __forceinline__ void mod_load_window(double* lds, const double* src, int W) {
+  const int tid = threadIdx.x;
+  const auto rs = mod_rsrc(src);
+  double v[MAXP];
+#pragma unroll
+  for (int r = 0; r < MAXP; ++r)
+    if ((r + 1) * NT <= W || tid + r * NT < W)
+      v[r] = __builtin_bit_cast(double,
+                                __builtin_amdgcn_raw_buffer_load_b64(rs, tid * 8, r * NT * 8, 0));
+#pragma unroll
+  for (int r = 0; r < MAXP; ++r)
+    if ((r + 1) * NT <= W || tid + r * NT < W) lds[tid + r * NT] = v[r];
+}
+__device__ __forceinline__ void mod_store2(double* base, int off, double a, double b) {
+  const jwv_u32x4 v = __builtin_bit_cast(jwv_u32x4, make_double2(a, b));
+  __builtin_amdgcn_raw_buffer_store_b128(v, mod_rsrc(base), off * 8, 0, 0);
+}
+
+// Run form of a level (M > 1): a lane computes M output pairs whose slots
+// (16-B units) are h = st/2 apart (st = 1: M adjacent pairs).  Pair slot s
+// reads tap slots s + l*h (inverse) or s - l*h (forward), so the M pairs
+// share all but M + L - 1 of their M*L 16-B LDS reads per operand (st = 1:
+// M + L/2 reads).  Lanes take (block, residue) = (t / h, t % h), a block
+// covering M*h slots: the 16 lanes of a ds_read_b128 group then sit at
+// distinct slots mod 16 for odd M, so the reads stay conflict-free at every
+// stride.  Summation order per output is the P2/one-output kernels' order.
+template <int L, int M>
+struct ModRun {
+  static_assert((M & 1) == 1 && L % 2 == 0, "odd M, even L");
+  template <int st>
+  static constexpr int h() { return st >= 2 ? st / 2 : 1; }
+  template <int st>
+  static constexpr int nrd() { return st == 1 ? M + L / 2 : M + L - 1; }
+  template <int st>
+  __device__ __forceinline__ static int slot0(int t) {
+    constexpr int H = h<st>();
+    return (t / H) * (M * H) + (t % H);
+  }
+};
+
 // ---------------------------------------------------------------- forward
 // Window: T outputs + left halo S of V_{J0-1}.  After level j the window
 // still carries Sn(j) = (L-1)(2^J1 - 2^j) halo samples; level j's outputs are
@@ -37,6 +85,23 @@ struct ModFwd1Geo {
   static constexpr int e0(int j) { return S - Sn(j); }
   static constexpr int nout(int j) { return T + Sn(j); }
   static constexpr int lds_doubles() { return W + 8; }  // + pad and one pair past the end
+  // Run form (ModRun, M pairs per lane): level j reads up to window index
+  // e0(j) + 2*NB*M*h (past its last output slot, NB run blocks of M*h slots)
+  static constexpr int kPad = (S & 1) ? 1 : 2;
+  static constexpr int run_reach(int j, int M) {
+    const int st = 1 << (j - 1), h = st >= 2 ? st / 2 : 1;
+    const int ns = nout(j) / 2, nb = (ns + M * h - 1) / (M * h);
+    return kPad + e0(j) + 2 * nb * M * h;
+  }
+  static constexpr int lds_doubles(int M) {
+    int b = lds_doubles();
+    if (M % 100 > 1)
+      for (int j = J0; j <= J1; ++j) {
+        const int r = run_reach(j, M % 100) + 2;
+        if (r > b) b = r;
+      }
+    return b;
+  }
 };
 
 // P2: a lane computes two adjacent outputs (e, e+1) with e of the parity of
@@ -45,9 +110,12 @@ struct ModFwd1Geo {
 // + e0 even, so every tap pair (e - l*st, e + 1 - l*st) is one 16-B LDS read
 // (st = 1: the 10-value run e-8 .. e+1) at a 16-B lane stride, and the W
 // pair (t0 - S + e even) is one 16-B store when the rows are 16-B aligned.
-template <int L, int NT, int T, int J0, int J1, bool FMA, int j, bool P2>
+template <int L, int NT, int T, int J0, int J1, bool FMA, int j, bool P2, int M = 1>
 struct ModFwd1Level {
-  static constexpr int kPad = (ModFwd1Geo<L, T, J0, J1>::S & 1) ? 1 : 2;
+  static constexpr int kPad = ModFwd1Geo<L, T, J0, J1>::kPad;
+  // M = m + 100*jr: run form with m pairs per lane on levels j >= jr
+  static constexpr int kM = M % 100, kJR = M / 100;
+  static constexpr bool kRun = kM > 1 && j >= kJR;
   __device__ __forceinline__ static void run_p2(const ModwtTaps<L>& tp, double* lds,
                                                 double* __restrict__ wout, int64_t ldw,
                                                 int64_t t0, int64_t N) {
@@ -61,6 +129,8 @@ struct ModFwd1Level {
     double* __restrict__ wrow = wout + (int64_t)(j - 1) * ldw + (t0 - G::S);
     // 16-B W stores: row base (j-1)*ldw + t0 - S + e is even for these e
     const bool w16 = (((uintptr_t)wrow + 8 * e0) & 15) == 0;
+    // the whole tile inside the signal and 16-B rows: buffer stores
+    const bool wfast = w16 && t0 + T <= N;
     double2 vv[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -105,7 +175,9 @@ struct ModFwd1Level {
       const int ee = e0 + 2 * k;  // S has e0's parity: a pair is all halo or all own
       if ((full || k < NP) && e0 + 2 * (r + 1) * NT > G::S && ee >= G::S) {
         const int64_t g = t0 + (ee - G::S);
-        if (w16 && g + 1 < N) {
+        if (wfast) {
+          mod_store2(wrow, ee, sw0, sw1);
+        } else if (w16 && g + 1 < N) {
           *reinterpret_cast<double2*>(wrow + ee) = make_double2(sw0, sw1);
         } else {
           if (g < N) wrow[ee] = sw0;
@@ -125,12 +197,103 @@ struct ModFwd1Level {
     }
     lds_barrier();
     if constexpr (j < J1)
-      ModFwd1Level<L, NT, T, J0, J1, FMA, j + 1, P2>::run(tp, lds, wout, ldw, t0, N);
+      ModFwd1Level<L, NT, T, J0, J1, FMA, j + 1, P2, M>::run(tp, lds, wout, ldw, t0, N);
+  }
+  // Run form (ModRun): output pair slot s = s0 + m*h, m < M (slot s = window
+  // outputs e0 + 2s, e0 + 2s + 1), reads tap slots s0 + (k - (L-1))*h,
+  // k < M + L - 1 (st = 1: window doubles e0 + 2*s0 - L .. e0 + 2*s0 + 2M - 1).
+  __device__ __forceinline__ static void run_mr(const ModwtTaps<L>& tp, double* lds,
+                                                double* __restrict__ wout, int64_t ldw,
+                                                int64_t t0, int64_t N) {
+    using G = ModFwd1Geo<L, T, J0, J1>;
+    constexpr int st = 1 << (j - 1);
+    constexpr int H = ModRun<L, kM>::template h<st>();
+    constexpr int NRD = ModRun<L, kM>::template nrd<st>();
+    constexpr int e0 = G::e0(j), nout = G::nout(j);
+    static_assert(((kPad + e0) & 1) == 0 && (nout & 1) == 0, "pairs must tile the outputs");
+    constexpr int NS = nout / 2;
+    constexpr int NB = (NS + kM * H - 1) / (kM * H);
+    constexpr int NTASK = NB * H;
+    constexpr int R = (NTASK + NT - 1) / NT;
+    static_assert(G::run_reach(j, kM) <= G::lds_doubles(M), "run reads past the window");
+    const int tid = opaque_tid();
+    double* __restrict__ wrow = wout + (int64_t)(j - 1) * ldw + (t0 - G::S);
+    const bool w16 = (((uintptr_t)wrow + 8 * e0) & 15) == 0;
+    double* const B = lds + kPad + e0;  // slot 0 of this level, 16-B aligned
+    double2 vv[R][kM];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int t = tid + r * NT;
+      const bool full = (r + 1) * NT <= NTASK;
+      // a wave whose tasks all lie past NTASK skips the slot (scalar branch)
+      if (!full && __builtin_amdgcn_readfirstlane((tid & ~63) + r * NT) >= NTASK) continue;
+      const int tc = full ? t : (t < NTASK ? t : NTASK - 1);
+      const int s0 = ModRun<L, kM>::template slot0<st>(tc);
+      double v[2 * NRD];
+      const double* rb = st == 1 ? B + 2 * s0 - L : B + 2 * s0 - 2 * (L - 1) * H;
+#pragma unroll
+      for (int k = 0; k < NRD; ++k) {
+        const double2 u = *reinterpret_cast<const double2*>(rb + 2 * k * H);
+        v[2 * k] = u.x;
+        v[2 * k + 1] = u.y;
+      }
+      double sw[kM][2], sv[kM][2];
+#pragma unroll
+      for (int m = 0; m < kM; ++m) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          double a = 0.0, c = 0.0;
+#pragma unroll
+          for (int l = 0; l < L; ++l) {
+            const double x = st == 1 ? v[2 * m + q - l + L] : v[2 * (m - l + L - 1) + q];
+            a = mac<FMA>(a, x, tp.h[l]);
+            c = mac<FMA>(c, x, tp.g[l]);
+          }
+          pin2(a, c);
+          sw[m][q] = a;
+          sv[m][q] = c;
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < kM; ++m) {
+        vv[r][m] = make_double2(sv[m][0], sv[m][1]);
+        const int s = s0 + m * H;
+        const int ee = e0 + 2 * s;  // S has e0's parity: a pair is all halo or all own
+        if ((full || t < NTASK) && s < NS && ee >= G::S) {
+          const int64_t g = t0 + (ee - G::S);
+          if (w16 && g + 1 < N) {
+            *reinterpret_cast<double2*>(wrow + ee) = make_double2(sw[m][0], sw[m][1]);
+          } else {
+            if (g < N) wrow[ee] = sw[m][0];
+            if (g + 1 < N) wrow[ee + 1] = sw[m][1];
+          }
+        }
+      }
+      asm volatile("" ::: "memory");  // slot fence
+    }
+    lds_barrier();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int t = tid + r * NT;
+      const bool ok = (r + 1) * NT <= NTASK || t < NTASK;
+      const int s0 = ModRun<L, kM>::template slot0<st>(ok ? t : 0);
+#pragma unroll
+      for (int m = 0; m < kM; ++m) {
+        const int s = s0 + m * H;
+        if (ok && s < NS) *reinterpret_cast<double2*>(B + 2 * s) = vv[r][m];
+      }
+    }
+    lds_barrier();
+    if constexpr (j < J1)
+      ModFwd1Level<L, NT, T, J0, J1, FMA, j + 1, P2, M>::run(tp, lds, wout, ldw, t0, N);
   }
   __device__ __forceinline__ static void run(const ModwtTaps<L>& tp, double* lds,
                                              double* __restrict__ wout, int64_t ldw, int64_t t0,
                                              int64_t N) {
-    if constexpr (P2) {
+    if constexpr (kRun) {
+      run_mr(tp, lds, wout, ldw, t0, N);
+      return;
+    } else if constexpr (P2) {
       run_p2(tp, lds, wout, ldw, t0, N);
       return;
     }
@@ -175,13 +338,13 @@ struct ModFwd1Level {
     }
     lds_barrier();
     if constexpr (j < J1)
-      ModFwd1Level<L, NT, T, J0, J1, FMA, j + 1, P2>::run(tp, lds, wout, ldw, t0, N);
+      ModFwd1Level<L, NT, T, J0, J1, FMA, j + 1, P2, M>::run(tp, lds, wout, ldw, t0, N);
   }
 };
 
 // src = V_{J0-1} (length N); W_j -> wout + (j-1)*ldw; V_{J1} -> vout.
 // Grid: ceil(N/T) blocks (XCD-aware order, xcd_tile).
-template <int L, int NT, int T, int J0, int J1, bool FMA, bool P2 = false>
+template <int L, int NT, int T, int J0, int J1, bool FMA, bool P2 = false, int M = 1>
 __global__ __launch_bounds__(NT) void modwt_fwd_tile1(const double* __restrict__ src,
                                                       double* __restrict__ wout, int64_t ldw,
                                                       double* __restrict__ vout, int64_t N,
@@ -189,19 +352,78 @@ __global__ __launch_bounds__(NT) void modwt_fwd_tile1(const double* __restrict__
   extern __shared__ __attribute__((aligned(16))) double lds[];
   using G = ModFwd1Geo<L, T, J0, J1>;
   constexpr int MAXP = (G::W + NT - 1) / NT;
-  constexpr int pad = P2 ? ModFwd1Level<L, NT, T, J0, J1, FMA, J0, P2>::kPad : 0;
+  constexpr int pad = (P2 || M % 100 > 1) ? G::kPad : 0;
   const int64_t t0 = xcd_tile() * T;
   const bool inside = t0 - G::S >= 0 && t0 + T <= N;  // block-uniform: no wrap
-  load_window<1, NT, MAXP>(lds + pad, src, G::W, false, 0, 1, [&](int e) {
-    return inside ? t0 - G::S + e : wrap_mod(t0 - G::S + e, N);
-  });
+  if (inside)
+    mod_load_window<NT, MAXP>(lds + pad, src + (t0 - G::S), G::W);
+  else
+    load_window<1, NT, MAXP>(lds + pad, src, G::W, false, 0, 1,
+                             [&](int e) { return wrap_mod(t0 - G::S + e, N); });
   lds_barrier();
-  ModFwd1Level<L, NT, T, J0, J1, FMA, J0, P2>::run(tp, lds, wout, ldw, t0, N);
+  ModFwd1Level<L, NT, T, J0, J1, FMA, J0, P2, M>::run(tp, lds, wout, ldw, t0, N);
   const int tid = threadIdx.x;
 #pragma unroll
   for (int r = 0; r < (T + NT - 1) / NT; ++r) {
     const int p = tid + r * NT;
     if (p < T && t0 + p < N) vout[t0 + p] = lds[pad + G::S + p];
+  }
+}
+
+// Persistent form of modwt_fwd_tile1: one block per CU walks the tiles of its
+// XCD's contiguous chunk (the chunk's blocks side by side, so a tile's halo is
+// a sibling's samples in the same L2) and loads the NEXT tile's window into
+// registers (buffer loads, in flight through all of this tile's levels) right
+// after this tile's window is in LDS: at one 80-KB block per CU the window load
+// is otherwise exposed at every tile start.  Same levels, same outputs.
+// Grid: 8 * blocks per XCD.
+template <int L, int NT, int T, int J0, int J1, bool FMA, bool P2 = false, int M = 1>
+__global__ __launch_bounds__(NT) void modwt_fwd_tile1p(const double* __restrict__ src,
+                                                       double* __restrict__ wout, int64_t ldw,
+                                                       double* __restrict__ vout, int64_t N,
+                                                       ModwtTaps<L> tp) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  using G = ModFwd1Geo<L, T, J0, J1>;
+  constexpr int MAXP = (G::W + NT - 1) / NT;
+  constexpr int pad = (P2 || M % 100 > 1) ? G::kPad : 0;
+  const int tid = threadIdx.x;
+  const int64_t ntile = (N + T - 1) / T;
+  const int x = blockIdx.x & 7, nbx = gridDim.x >> 3, bx = blockIdx.x >> 3;
+  const int64_t q = ntile >> 3, rr = ntile & 7;
+  const int64_t c0 = x * q + (x < rr ? x : rr), c1 = c0 + q + (x < rr ? 1 : 0);
+  auto inside_at = [&](int64_t t0) { return t0 - G::S >= 0 && t0 + T <= N; };
+  double pv[MAXP];
+  bool have = false;
+  for (int64_t tile = c0 + bx; tile < c1; tile += nbx) {
+    const int64_t t0 = tile * T;
+    if (have) {
+#pragma unroll
+      for (int r = 0; r < MAXP; ++r)
+        if ((r + 1) * NT <= G::W || tid + r * NT < G::W) lds[pad + tid + r * NT] = pv[r];
+    } else if (inside_at(t0)) {
+      mod_load_window<NT, MAXP>(lds + pad, src + (t0 - G::S), G::W);
+    } else {
+      load_window<1, NT, MAXP>(lds + pad, src, G::W, false, 0, 1,
+                               [&](int e) { return wrap_mod(t0 - G::S + e, N); });
+    }
+    lds_barrier();
+    const int64_t tn = tile + nbx;
+    have = tn < c1 && inside_at(tn * T);
+    if (have) {
+      const auto rs = mod_rsrc(src + (tn * T - G::S));
+#pragma unroll
+      for (int r = 0; r < MAXP; ++r)
+        if ((r + 1) * NT <= G::W || tid + r * NT < G::W)
+          pv[r] = __builtin_bit_cast(
+              double, __builtin_amdgcn_raw_buffer_load_b64(rs, tid * 8, r * NT * 8, 0));
+    }
+    ModFwd1Level<L, NT, T, J0, J1, FMA, J0, P2, M>::run(tp, lds, wout, ldw, t0, N);
+#pragma unroll
+    for (int r = 0; r < (T + NT - 1) / NT; ++r) {
+      const int p = tid + r * NT;
+      if (p < T && t0 + p < N) vout[t0 + p] = lds[pad + G::S + p];
+    }
+    lds_barrier();  // LDS reuse by the next tile
   }
 }
 
@@ -217,11 +439,31 @@ struct ModInv1Geo {
   static constexpr int Wmax = T + Rin(J1);
   static constexpr int buf() { return (Wmax + 4) & ~1; }  // + one pair read past the end (P2)
   static constexpr int lds_doubles() { return 2 * buf(); }
+  // Run form (M pairs per lane, ModRun): the last run block of level j reads
+  // up to 2*NB*M*h + (L-1)*st doubles (st = 1: 2*NB*M + L) of each buffer.
+  static constexpr int nout(int j) { return T + Rout(j); }
+  static constexpr int run_reach(int j, int M) {
+    const int st = 1 << (j - 1), h = st >= 2 ? st / 2 : 1;
+    const int ns = (nout(j) + 1) / 2, nb = (ns + M * h - 1) / (M * h);
+    return st == 1 ? 2 * nb * M + L : 2 * nb * M * h + (L - 1) * st;
+  }
+  static constexpr int run_buf(int M) {
+    int b = buf();
+    for (int j = J0; j <= J1; ++j) {
+      const int r = (run_reach(j, M % 100) + 3) & ~1;
+      if (r > b) b = r;
+    }
+    return b;
+  }
+  static constexpr int lds_doubles(int M) { return M % 100 > 1 ? 2 * run_buf(M) : lds_doubles(); }
 };
 
-template <int L, int NT, int T, int J0, int J1, bool FMA, int j, bool P2 = false>
+
+template <int L, int NT, int T, int J0, int J1, bool FMA, int j, bool P2 = false, int M = 1>
 struct ModInv1Level {
   using G = ModInv1Geo<L, T, J0, J1>;
+  static constexpr int kM = M % 100, kJR = M / 100;
+  static constexpr bool kRun = kM > 1 && j >= kJR;
   static constexpr int MAXP = (G::Wmax + NT - 1) / NT;
   // fetch the W_j window [t0, t0 + T + Rin(j)) into registers
   __device__ __forceinline__ static void fetch(double (&pw)[MAXP], const double* __restrict__ coef,
@@ -229,11 +471,24 @@ struct ModInv1Level {
     constexpr int Wn = T + G::Rin(j);
     const double* row = coef + (int64_t)(j - 1) * ldw;
     const int tid = opaque_tid();
+    if (inside) {
+      // buffer loads: block-uniform base in SGPRs, one lane offset, the slot
+      // offsets r*NT*8 as scalar offsets (no per-load 64-bit address VALU)
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(row + t0), 0,
+                                                        0x7ffffff0, 0x00020000);
+#pragma unroll
+      for (int r = 0; r < MAXP; ++r) {
+        const int q = tid + r * NT;
+        if (r * NT < Wn && ((r + 1) * NT <= Wn || q < Wn))
+          pw[r] = __builtin_bit_cast(
+              double, __builtin_amdgcn_raw_buffer_load_b64(rs, tid * 8, r * NT * 8, 0));
+      }
+      return;
+    }
 #pragma unroll
     for (int r = 0; r < MAXP; ++r) {
       const int q = tid + r * NT;
-      if (r * NT < Wn && ((r + 1) * NT <= Wn || q < Wn))
-        pw[r] = row[inside ? t0 + q : wrap_mod(t0 + q, N)];
+      if (r * NT < Wn && ((r + 1) * NT <= Wn || q < Wn)) pw[r] = row[wrap_mod(t0 + q, N)];
     }
   }
   __device__ __forceinline__ static void run(const ModwtTaps<L>& tp, double* vb, double* wb,
@@ -251,8 +506,11 @@ struct ModInv1Level {
     }
     lds_barrier();
     if constexpr (j > J0)
-      ModInv1Level<L, NT, T, J0, J1, FMA, j - 1, P2>::fetch(pw, coef, ldw, t0, N, inside);
-    if constexpr (P2) {
+      ModInv1Level<L, NT, T, J0, J1, FMA, j - 1, P2, M>::fetch(pw, coef, ldw, t0, N, inside);
+    if constexpr (kRun) {
+      compute_mr(tp, vb, wb, pw, coef, ldw, dst, t0, N, inside);
+      return;
+    } else if constexpr (P2) {
       compute_p2(tp, vb, wb, pw, coef, ldw, dst, t0, N, inside);
       return;
     }
@@ -295,7 +553,7 @@ struct ModInv1Level {
         if ((r + 1) * NT <= nout || p < nout) vb[p] = vv[r];
       }
       // (the barrier after the next level's W write orders these)
-      ModInv1Level<L, NT, T, J0, J1, FMA, j - 1, P2>::run(tp, vb, wb, pw, coef, ldw, dst, t0, N,
+      ModInv1Level<L, NT, T, J0, J1, FMA, j - 1, P2, M>::run(tp, vb, wb, pw, coef, ldw, dst, t0, N,
                                                           inside);
     }
   }
@@ -386,29 +644,124 @@ struct ModInv1Level {
         const int k = tid + r * NT;
         if ((r + 1) * NT <= NP || k < NP) *reinterpret_cast<double2*>(vb + 2 * k) = vv[r];
       }
-      ModInv1Level<L, NT, T, J0, J1, FMA, j - 1, P2>::run(tp, vb, wb, pw, coef, ldw, dst, t0, N,
+      ModInv1Level<L, NT, T, J0, J1, FMA, j - 1, P2, M>::run(tp, vb, wb, pw, coef, ldw, dst, t0, N,
                                                           inside);
     }
+  }
+  // Run form (ModRun): output pair slot s = s0 + m*h, m < M, reads tap slots
+  // s0 + k*h, k < M + L - 1 (st = 1: doubles 2*s0 .. 2*s0 + 2M + L - 1).
+  // V taps first, then W taps (registers: one operand's run at a time).
+  template <bool ISW>
+  __device__ __forceinline__ static void run_sums(const ModwtTaps<L>& tp, const double* base,
+                                                  double (&acc)[kM][2]) {
+    constexpr int st = 1 << (j - 1);
+    constexpr int H = ModRun<L, kM>::template h<st>();
+    constexpr int NRD = ModRun<L, kM>::template nrd<st>();
+    double v[2 * NRD];
+#pragma unroll
+    for (int k = 0; k < NRD; ++k) {
+      const double2 u = *reinterpret_cast<const double2*>(base + 2 * k * H);
+      v[2 * k] = u.x;
+      v[2 * k + 1] = u.y;
+    }
+#pragma unroll
+    for (int m = 0; m < kM; ++m) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        double s = 0.0;
+#pragma unroll
+        for (int l = 0; l < L; ++l) {
+          // st = 1: output 2(s0+m)+q, tap l -> double 2m + q + l of the run;
+          // st >= 2: slot m + l of the run, half q
+          const double x = st == 1 ? v[2 * m + q + l] : v[2 * (m + l) + q];
+          s = mac<FMA>(s, x, ISW ? tp.h[l] : tp.g[l]);
+        }
+        acc[m][q] = s;
+      }
+    }
+  }
+  __device__ __forceinline__ static void compute_mr(const ModwtTaps<L>& tp, double* vb, double* wb,
+                                                    double (&pw)[MAXP],
+                                                    const double* __restrict__ coef, int64_t ldw,
+                                                    double* __restrict__ dst, int64_t t0,
+                                                    int64_t N, bool inside) {
+    constexpr int st = 1 << (j - 1);
+    constexpr int H = ModRun<L, kM>::template h<st>();
+    constexpr int nout = G::nout(j);
+    constexpr int NS = (nout + 1) / 2;  // output pair slots
+    constexpr int NB = (NS + kM * H - 1) / (kM * H);
+    constexpr int NTASK = NB * H;
+    constexpr int R = (NTASK + NT - 1) / NT;
+    static_assert(G::run_reach(j, kM) <= G::run_buf(M), "run reads past the buffer");
+    const int tid = opaque_tid();
+    double2 vv[R][kM];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int t = tid + r * NT;
+      const bool full = (r + 1) * NT <= NTASK;
+      // a wave whose tasks all lie past NTASK skips the slot (scalar branch)
+      if (!full && __builtin_amdgcn_readfirstlane((tid & ~63) + r * NT) >= NTASK) continue;
+      const int tc = full ? t : (t < NTASK ? t : NTASK - 1);
+      const int s0 = ModRun<L, kM>::template slot0<st>(tc);
+      double sa[kM][2], sd[kM][2];
+      run_sums<false>(tp, vb + 2 * s0, sa);
+      run_sums<true>(tp, wb + 2 * s0, sd);
+#pragma unroll
+      for (int m = 0; m < kM; ++m) {
+        pin2(sa[m][0], sd[m][0]);
+        pin2(sa[m][1], sd[m][1]);
+        vv[r][m] = make_double2(sa[m][0] + sd[m][0], sa[m][1] + sd[m][1]);
+      }
+      asm volatile("" ::: "memory");  // slot fence
+    }
+    lds_barrier();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int t = tid + r * NT;
+      const bool ok = (r + 1) * NT <= NTASK || t < NTASK;
+      const int s0 = ModRun<L, kM>::template slot0<st>(ok ? t : 0);
+#pragma unroll
+      for (int m = 0; m < kM; ++m) {
+        const int s = s0 + m * H;
+        if constexpr (j == J0) {
+          const int p = 2 * s;
+          if (ok && p < T) {
+            if (t0 + p + 1 < N && p + 1 < T) {
+              *reinterpret_cast<double2*>(dst + t0 + p) = vv[r][m];
+            } else if (t0 + p < N) {
+              dst[t0 + p] = vv[r][m].x;
+            }
+          }
+        } else {
+          if (ok && s < NS) *reinterpret_cast<double2*>(vb + 2 * s) = vv[r][m];
+        }
+      }
+    }
+    if constexpr (j > J0)
+      ModInv1Level<L, NT, T, J0, J1, FMA, j - 1, P2, M>::run(tp, vb, wb, pw, coef, ldw, dst, t0, N,
+                                                          inside);
   }
 };
 
 // vsrc = V_{J1}; W_j at coef + (j-1)*ldw; output V_{J0-1} -> dst.
-template <int L, int NT, int T, int J0, int J1, bool FMA, bool P2 = false>
+template <int L, int NT, int T, int J0, int J1, bool FMA, bool P2 = false, int M = 1>
 __global__ __launch_bounds__(NT) void modwt_inv_tile1(const double* __restrict__ vsrc,
                                                       const double* __restrict__ coef, int64_t ldw,
                                                       double* __restrict__ dst, int64_t N,
                                                       ModwtTaps<L> tp) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   using G = ModInv1Geo<L, T, J0, J1>;
-  using Top = ModInv1Level<L, NT, T, J0, J1, FMA, J1, P2>;
+  using Top = ModInv1Level<L, NT, T, J0, J1, FMA, J1, P2, M>;
   double* vb = lds;
-  double* wb = lds + G::buf();
+  double* wb = lds + (M % 100 > 1 ? G::run_buf(M) : G::buf());
   const int64_t t0 = xcd_tile() * T;
   const bool inside = t0 + G::Wmax <= N;
   double pw[Top::MAXP];
-  load_window<1, NT, Top::MAXP>(vb, vsrc, G::Wmax, false, 0, 1, [&](int e) {
-    return inside ? t0 + e : wrap_mod(t0 + e, N);
-  });
+  if (inside)
+    mod_load_window<NT, Top::MAXP>(vb, vsrc + t0, G::Wmax);
+  else
+    load_window<1, NT, Top::MAXP>(vb, vsrc, G::Wmax, false, 0, 1,
+                                  [&](int e) { return wrap_mod(t0 + e, N); });
   Top::fetch(pw, coef, ldw, t0, N, inside);
   Top::run(tp, vb, wb, pw, coef, ldw, dst, t0, N, inside);
 }
