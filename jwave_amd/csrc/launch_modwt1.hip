@@ -55,12 +55,15 @@ hipError_t fwd_kp(const Bank& b, const ModwtArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.wout, a.ldw, a.vout, a.N, taps<L>(b));
   return hipGetLastError();
 }
-// Persistent forward (modwt_fwd_tile1p): blocks per CU x CUs, rounded to a
-// multiple of 8 (XCDs); env JWV_MODWT_PF = 0 keeps the one-tile-per-block grid
+// Persistent tiles (modwt_fwd_tile1p / modwt_inv_tile1p): blocks per CU x
+// CUs, a multiple of 8 (XCDs); env JWV_MODWT_PF bit 0 forward, bit 1 inverse
+// (a clear bit keeps the one-tile-per-block grid).  Off by default: r03, one
+// box, two rounds: forward 169.2 / 169.6 us one tile per block vs 200.3 /
+// 201.3 persistent; inverse (303) 225.0 / 226.8 vs 243.2 / 246.6.
 int pf_env() {
   static const int v = [] {
     const char* e = std::getenv("JWV_MODWT_PF");
-    return e ? std::atoi(e) : 1;
+    return e ? std::atoi(e) : 0;
   }();
   return v;
 }
@@ -86,6 +89,21 @@ hipError_t fwd_kpp(const Bank& b, const ModwtArgs& a, hipStream_t s) {
   if (nb > need) nb = need;
   if (nb < 1) nb = 1;
   hipLaunchKernelGGL(k, dim3((unsigned)(8 * nb)), dim3(NT), lds, s, a.src, a.wout, a.ldw, a.vout,
+                     a.N, taps<L>(b));
+  return hipGetLastError();
+}
+template <int L, int J1, int NT, int TI, int M = 1>
+hipError_t inv_kpp(const Bank& b, const ModwtArgs& a, hipStream_t s) {
+  auto k = modwt_inv_tile1p<L, NT, TI, 1, J1, kFMA, true, M>;
+  const size_t lds = (size_t)ModInv1Geo<L, TI, 1, J1>::lds_doubles(M) * sizeof(double);
+  if (hipError_t e = prep(k, lds)) return e;
+  const int64_t ntile = (a.N + TI - 1) / TI;
+  const int per_cu = (int)(163840 / (lds + 1024));  // LDS-bound blocks per CU
+  int64_t nb = (int64_t)(cu_count() / 8) * (per_cu < 1 ? 1 : per_cu);
+  const int64_t need = (ntile + 7) / 8;
+  if (nb > need) nb = need;
+  if (nb < 1) nb = 1;
+  hipLaunchKernelGGL(k, dim3((unsigned)(8 * nb)), dim3(NT), lds, s, a.src, a.coef, a.ldw, a.vout,
                      a.N, taps<L>(b));
   return hipGetLastError();
 }
@@ -134,7 +152,7 @@ hipError_t fwd_k(const Bank& b, const ModwtArgs& a, hipStream_t s) {
       case 5: return fwd_kp<L, J1, true, 1024, 16384>(b, a, s);
       default:
         if (p2_bits() & 1) {
-          if (pf_env() == 1 && run_f() == 1) return fwd_kpp<L, J1, 1024, 8192>(b, a, s);
+          if ((pf_env() & 1) && run_f() == 1) return fwd_kpp<L, J1, 1024, 8192>(b, a, s);
           switch (run_f()) {
             case 3: return fwd_kp<L, J1, true, 1024, 8192, 3>(b, a, s);
             case 303: return fwd_kp<L, J1, true, 1024, 8192, 303>(b, a, s);
@@ -158,9 +176,15 @@ hipError_t inv_k(const Bank& b, const ModwtArgs& a, hipStream_t s) {
       case 4: return inv_kp<L, J1, true, 256, 2048>(b, a, s);
       default:
         if (p2_bits() & 2) {
+          if (pf_env() & 2) {
+            if (run_m() == 303) return inv_kpp<L, J1, kNT, kTI, 303>(b, a, s);
+            if (run_m() == 1303) return inv_kpp<L, J1, kNT, kTI, 1303>(b, a, s);
+            if (run_m() == 1) return inv_kpp<L, J1, kNT, kTI>(b, a, s);
+          }
           switch (run_m()) {
             case 3: return inv_kp<L, J1, true, kNT, kTI, 3>(b, a, s);
             case 303: return inv_kp<L, J1, true, kNT, kTI, 303>(b, a, s);
+            case 1303: return inv_kp<L, J1, true, kNT, kTI, 1303>(b, a, s);
             case 503: return inv_kp<L, J1, true, kNT, kTI, 503>(b, a, s);
             default: break;
           }

@@ -37,9 +37,21 @@ hipError_t wfwd1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a.src, a.sv, a.dst, a.dv, a.h, tp);
   return hipGetLastError();
 }
-template <int L, int K>
+// env JWV_WPT_ILV (default 1): the reverse tiles' couples as four interleaved
+// sums (rev_couple_ilv); 0 = two rev_pair calls
+bool wpt_ilv() {
+  static const bool v = [] {
+    const char* e = std::getenv("JWV_WPT_ILV");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+template <int L, int K, bool ILV = false>
 hipError_t wrev1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
-  auto k = wpt_rev_tile1<L, 256, kWptT, K, kFMA>;
+  if constexpr (!ILV && L >= 8) {
+    if (wpt_ilv()) return wrev1_k<L, K, true>(b, a, s);
+  }
+  auto k = wpt_rev_tile1<L, 256, kWptT, K, kFMA, ILV>;
   const size_t lds = (size_t)Wpt1RevGeo<L, kWptT, K>::lds_doubles() * sizeof(double);
   if (hipError_t e = prep1(k, lds)) return e;
   RevTaps<L> tp;
@@ -52,12 +64,25 @@ hipError_t wrev1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
 // 4096 tile (14.7% -> 7.4% extra pairs) at the same waves per CU.  Config 4
 // forward 2597 -> 2468 us; the reverse (halo ~7% at 4096) measured no gain
 // and keeps 4096.  env JWV_WPT8K=0: 4096 for both.
-template <int L, bool FWD>
+// env JWV_WPT_ILVF (default 0): the same interleaving in the 8192 forward
+// tiles (fwd_couple_ilv).  r03, one box, two rounds: forward 2498 / 2471 us
+// interleaved vs 2488 / 2454 (no gain; the reverse gains 2728 / 2752 -> 2702
+// / 2708 with JWV_WPT_ILV)
+bool wpt_ilvf() {
+  static const bool v = [] {
+    const char* e = std::getenv("JWV_WPT_ILVF");
+    return e ? std::atoi(e) != 0 : false;
+  }();
+  return v;
+}
+template <int L, bool FWD, bool ILV = false>
 hipError_t wpt8k(const Bank& b, const TileArgs& a, hipStream_t s) {
   constexpr int TT = 8192, K = 6;
   const dim3 grid((unsigned)(a.nouter * (a.h / TT)));
   if constexpr (FWD) {
-    auto k = wpt_fwd_tile1<L, 512, TT, K, kFMA>;
+    if constexpr (!ILV && L >= 8)
+      if (wpt_ilvf()) return wpt8k<L, true, true>(b, a, s);
+    auto k = wpt_fwd_tile1<L, 512, TT, K, kFMA, ILV>;
     const size_t lds = (size_t)Wpt1FwdGeo<L, TT, K>::lds_doubles() * sizeof(double);
     if (hipError_t e = prep1(k, lds)) return e;
     FwdTaps<L> tp;

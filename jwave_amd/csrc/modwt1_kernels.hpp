@@ -448,6 +448,7 @@ struct ModInv1Geo {
     return st == 1 ? 2 * nb * M + L : 2 * nb * M * h + (L - 1) * st;
   }
   static constexpr int run_buf(int M) {
+    M %= 1000;
     int b = buf();
     for (int j = J0; j <= J1; ++j) {
       const int r = (run_reach(j, M % 100) + 3) & ~1;
@@ -455,14 +456,18 @@ struct ModInv1Geo {
     }
     return b;
   }
-  static constexpr int lds_doubles(int M) { return M % 100 > 1 ? 2 * run_buf(M) : lds_doubles(); }
+  static constexpr int lds_doubles(int M) {
+    return M % 100 > 1 ? 2 * run_buf(M) : lds_doubles();
+  }
 };
 
 
 template <int L, int NT, int T, int J0, int J1, bool FMA, int j, bool P2 = false, int M = 1>
 struct ModInv1Level {
   using G = ModInv1Geo<L, T, J0, J1>;
-  static constexpr int kM = M % 100, kJR = M / 100;
+  // M = m + 100*jr (+ 1000: tap-major interleaved run sums, run_sums_ilv)
+  static constexpr int kM = M % 100, kJR = (M / 100) % 10;
+  static constexpr bool kILV = M >= 1000;
   static constexpr bool kRun = kM > 1 && j >= kJR;
   static constexpr int MAXP = (G::Wmax + NT - 1) / NT;
   // fetch the W_j window [t0, t0 + T + Rin(j)) into registers
@@ -494,7 +499,8 @@ struct ModInv1Level {
   __device__ __forceinline__ static void run(const ModwtTaps<L>& tp, double* vb, double* wb,
                                              double (&pw)[MAXP], const double* __restrict__ coef,
                                              int64_t ldw, double* __restrict__ dst, int64_t t0,
-                                             int64_t N, bool inside) {
+                                             int64_t N, bool inside, int64_t tn = -1,
+      bool inn = false) {
     constexpr int st = 1 << (j - 1);
     constexpr int Wn = T + G::Rin(j), nout = T + G::Rout(j);
     constexpr int R = (nout + NT - 1) / NT;
@@ -507,11 +513,13 @@ struct ModInv1Level {
     lds_barrier();
     if constexpr (j > J0)
       ModInv1Level<L, NT, T, J0, J1, FMA, j - 1, P2, M>::fetch(pw, coef, ldw, t0, N, inside);
+    else if (tn >= 0)  // persistent form: the next tile's top W window
+      ModInv1Level<L, NT, T, J0, J1, FMA, J1, P2, M>::fetch(pw, coef, ldw, tn, N, inn);
     if constexpr (kRun) {
-      compute_mr(tp, vb, wb, pw, coef, ldw, dst, t0, N, inside);
+      compute_mr(tp, vb, wb, pw, coef, ldw, dst, t0, N, inside, tn, inn);
       return;
     } else if constexpr (P2) {
-      compute_p2(tp, vb, wb, pw, coef, ldw, dst, t0, N, inside);
+      compute_p2(tp, vb, wb, pw, coef, ldw, dst, t0, N, inside, tn, inn);
       return;
     }
     double vv[R];
@@ -554,7 +562,7 @@ struct ModInv1Level {
       }
       // (the barrier after the next level's W write orders these)
       ModInv1Level<L, NT, T, J0, J1, FMA, j - 1, P2, M>::run(tp, vb, wb, pw, coef, ldw, dst, t0, N,
-                                                          inside);
+                                                          inside, tn, inn);
     }
   }
   // P2: a lane computes the adjacent outputs (p, p+1), p even: every tap pair
@@ -565,7 +573,8 @@ struct ModInv1Level {
                                                     double (&pw)[MAXP],
                                                     const double* __restrict__ coef, int64_t ldw,
                                                     double* __restrict__ dst, int64_t t0,
-                                                    int64_t N, bool inside) {
+                                                    int64_t N, bool inside, int64_t tn = -1,
+      bool inn = false) {
     constexpr int st = 1 << (j - 1);
     constexpr int nout = T + G::Rout(j);
     constexpr int NP = (nout + 1) / 2;
@@ -645,7 +654,7 @@ struct ModInv1Level {
         if ((r + 1) * NT <= NP || k < NP) *reinterpret_cast<double2*>(vb + 2 * k) = vv[r];
       }
       ModInv1Level<L, NT, T, J0, J1, FMA, j - 1, P2, M>::run(tp, vb, wb, pw, coef, ldw, dst, t0, N,
-                                                          inside);
+                                                          inside, tn, inn);
     }
   }
   // Run form (ModRun): output pair slot s = s0 + m*h, m < M, reads tap slots
@@ -680,11 +689,44 @@ struct ModInv1Level {
       }
     }
   }
+  // run_sums with the tap loop outermost and every accumulator materialised
+  // after each tap: the 2*M independent chains stay interleaved (the compiler
+  // otherwise schedules them one after the other, each add waiting on the
+  // previous one).  Same per-output summation order.
+  template <bool ISW>
+  __device__ __forceinline__ static void run_sums_ilv(const ModwtTaps<L>& tp, const double* base,
+                                                      double (&acc)[kM][2]) {
+    constexpr int st = 1 << (j - 1);
+    constexpr int H = ModRun<L, kM>::template h<st>();
+    constexpr int NRD = ModRun<L, kM>::template nrd<st>();
+    double v[2 * NRD];
+#pragma unroll
+    for (int k = 0; k < NRD; ++k) {
+      const double2 u = *reinterpret_cast<const double2*>(base + 2 * k * H);
+      v[2 * k] = u.x;
+      v[2 * k + 1] = u.y;
+    }
+#pragma unroll
+    for (int m = 0; m < kM; ++m) acc[m][0] = acc[m][1] = 0.0;
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+#pragma unroll
+      for (int m = 0; m < kM; ++m)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const double x = st == 1 ? v[2 * m + q + l] : v[2 * (m + l) + q];
+          acc[m][q] = mac<FMA>(acc[m][q], x, ISW ? tp.h[l] : tp.g[l]);
+        }
+#pragma unroll
+      for (int m = 0; m < kM; ++m) pin2(acc[m][0], acc[m][1]);
+    }
+  }
   __device__ __forceinline__ static void compute_mr(const ModwtTaps<L>& tp, double* vb, double* wb,
                                                     double (&pw)[MAXP],
                                                     const double* __restrict__ coef, int64_t ldw,
                                                     double* __restrict__ dst, int64_t t0,
-                                                    int64_t N, bool inside) {
+                                                    int64_t N, bool inside, int64_t tn = -1,
+      bool inn = false) {
     constexpr int st = 1 << (j - 1);
     constexpr int H = ModRun<L, kM>::template h<st>();
     constexpr int nout = G::nout(j);
@@ -704,8 +746,13 @@ struct ModInv1Level {
       const int tc = full ? t : (t < NTASK ? t : NTASK - 1);
       const int s0 = ModRun<L, kM>::template slot0<st>(tc);
       double sa[kM][2], sd[kM][2];
-      run_sums<false>(tp, vb + 2 * s0, sa);
-      run_sums<true>(tp, wb + 2 * s0, sd);
+      if constexpr (kILV) {
+        run_sums_ilv<false>(tp, vb + 2 * s0, sa);
+        run_sums_ilv<true>(tp, wb + 2 * s0, sd);
+      } else {
+        run_sums<false>(tp, vb + 2 * s0, sa);
+        run_sums<true>(tp, wb + 2 * s0, sd);
+      }
 #pragma unroll
       for (int m = 0; m < kM; ++m) {
         pin2(sa[m][0], sd[m][0]);
@@ -739,7 +786,7 @@ struct ModInv1Level {
     }
     if constexpr (j > J0)
       ModInv1Level<L, NT, T, J0, J1, FMA, j - 1, P2, M>::run(tp, vb, wb, pw, coef, ldw, dst, t0, N,
-                                                          inside);
+                                                          inside, tn, inn);
   }
 };
 
@@ -764,6 +811,60 @@ __global__ __launch_bounds__(NT) void modwt_inv_tile1(const double* __restrict__
                                   [&](int e) { return wrap_mod(t0 + e, N); });
   Top::fetch(pw, coef, ldw, t0, N, inside);
   Top::run(tp, vb, wb, pw, coef, ldw, dst, t0, N, inside);
+}
+
+// Persistent form of modwt_inv_tile1 (as modwt_fwd_tile1p): blocks walk their
+// XCD's chunk of tiles; the next tile's V window is loaded into registers at
+// this tile's start and its top W window in this tile's last level, so both
+// are in flight while this tile computes.  Same levels, same outputs.
+template <int L, int NT, int T, int J0, int J1, bool FMA, bool P2 = false, int M = 1>
+__global__ __launch_bounds__(NT) void modwt_inv_tile1p(const double* __restrict__ vsrc,
+                                                       const double* __restrict__ coef, int64_t ldw,
+                                                       double* __restrict__ dst, int64_t N,
+                                                       ModwtTaps<L> tp) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  using G = ModInv1Geo<L, T, J0, J1>;
+  using Top = ModInv1Level<L, NT, T, J0, J1, FMA, J1, P2, M>;
+  constexpr int MAXP = Top::MAXP;
+  double* vb = lds;
+  double* wb = lds + (M % 100 > 1 ? G::run_buf(M) : G::buf());
+  const int tid = threadIdx.x;
+  const int64_t ntile = (N + T - 1) / T;
+  const int x = blockIdx.x & 7, nbx = gridDim.x >> 3, bx = blockIdx.x >> 3;
+  const int64_t q = ntile >> 3, rr = ntile & 7;
+  const int64_t c0 = x * q + (x < rr ? x : rr), c1 = c0 + q + (x < rr ? 1 : 0);
+  double pw[MAXP], pv[MAXP];
+  bool have = false;  // pv holds this tile's V window, pw its top W window
+  for (int64_t tile = c0 + bx; tile < c1; tile += nbx) {
+    const int64_t t0 = tile * T;
+    const bool inside = t0 + G::Wmax <= N;
+    if (have) {
+#pragma unroll
+      for (int r = 0; r < MAXP; ++r)
+        if ((r + 1) * NT <= G::Wmax || tid + r * NT < G::Wmax) vb[tid + r * NT] = pv[r];
+    } else {
+      if (inside)
+        mod_load_window<NT, MAXP>(vb, vsrc + t0, G::Wmax);
+      else
+        load_window<1, NT, MAXP>(vb, vsrc, G::Wmax, false, 0, 1,
+                                 [&](int e) { return wrap_mod(t0 + e, N); });
+      Top::fetch(pw, coef, ldw, t0, N, inside);
+    }
+    const int64_t tn = tile + nbx < c1 ? (tile + nbx) * T : -1;
+    have = tn >= 0 && tn + G::Wmax <= N;
+    if (have) {
+      const auto rs = mod_rsrc(vsrc + tn);
+#pragma unroll
+      for (int r = 0; r < MAXP; ++r)
+        if ((r + 1) * NT <= G::Wmax || tid + r * NT < G::Wmax)
+          pv[r] = __builtin_bit_cast(
+              double, __builtin_amdgcn_raw_buffer_load_b64(rs, tid * 8, r * NT * 8, 0));
+    }
+    // the last level fetches the next tile's top W window only when it is
+    // prefetched as a whole (have); otherwise the next tile loads both itself
+    Top::run(tp, vb, wb, pw, coef, ldw, dst, t0, N, inside, have ? tn : -1, true);
+    lds_barrier();  // LDS reuse by the next tile
+  }
 }
 
 }  // namespace jwv

@@ -32,7 +32,30 @@ struct Wpt1FwdGeo {
   static_assert((L & 1) == 0 && ((T >> K) & 1) == 0, "even windows");
 };
 
-template <int L, int NT, int T, int K, bool FMA, int l>
+// Couple (pairs i, i+1) of fwd_pair with the tap loop shared: x[j] = window
+// sample 2i + j; the four sums keep fwd_pair's per-output order (j ascending
+// from +0.0) and are materialised after every tap, so the four dependent add
+// chains stay interleaved (the compiler otherwise runs two, each add waiting on
+// the multiply it consumes and on the previous add).
+template <int L, bool FMA>
+__device__ __forceinline__ void fwd_couple_ilv(const FwdTaps<L>& tp, const double* x, double& a0,
+                                               double& d0, double& a1, double& d1) {
+  double sa0 = 0.0, sd0 = 0.0, sa1 = 0.0, sd1 = 0.0;
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    sa0 = mac<FMA>(sa0, x[j], FB<L>::lo(tp, j));
+    sd0 = mac<FMA>(sd0, x[j], FB<L>::hi(tp, j));
+    sa1 = mac<FMA>(sa1, x[j + 2], FB<L>::lo(tp, j));
+    sd1 = mac<FMA>(sd1, x[j + 2], FB<L>::hi(tp, j));
+    asm volatile("" : "+v"(sa0), "+v"(sd0), "+v"(sa1), "+v"(sd1));
+  }
+  a0 = sa0;
+  d0 = sd0;
+  a1 = sa1;
+  d1 = sd1;
+}
+
+template <int L, int NT, int T, int K, bool FMA, int l, bool ILV = false>
 struct Wpt1FwdLevel {
   // lds: 2^(l-1) input sub-windows of m(l-1) samples (stride m(l-1)).
   __device__ __forceinline__ static void run(const FwdTaps<L>& tp, double* lds, int h, int t,
@@ -59,8 +82,12 @@ struct Wpt1FwdLevel {
           x[j + 1] = v.y;
         }
         double a0, d0, a1, d1;
-        fwd_pair<L, FMA>(tp, [&](int j) { return x[j]; }, a0, d0);
-        fwd_pair<L, FMA>(tp, [&](int j) { return x[j + 2]; }, a1, d1);
+        if constexpr (ILV) {
+          fwd_couple_ilv<L, FMA>(tp, x, a0, d0, a1, d1);
+        } else {
+          fwd_pair<L, FMA>(tp, [&](int j) { return x[j]; }, a0, d0);
+          fwd_pair<L, FMA>(tp, [&](int j) { return x[j + 2]; }, a1, d1);
+        }
         // slot boundary: results exist here and later slots' LDS reads stay
         // below, so the compiler cannot hoist all slots' windows at once
         // (L = 16: ~190 VGPRs, 2 waves/SIMD -> ~80 VGPRs)
@@ -88,14 +115,14 @@ struct Wpt1FwdLevel {
         }
       }
       lds_barrier();
-      Wpt1FwdLevel<L, NT, T, K, FMA, l + 1>::run(tp, lds, h, t, y);
+      Wpt1FwdLevel<L, NT, T, K, FMA, l + 1, ILV>::run(tp, lds, h, t, y);
     }
   }
 };
 
 // Grid: rows * (h / T) blocks; row o = packet o of the pass input (view sv,
 // packets addressed through view_base); output rows likewise (view dv).
-template <int L, int NT, int T, int K, bool FMA>
+template <int L, int NT, int T, int K, bool FMA, bool ILV = false>
 __global__ __launch_bounds__(NT) void wpt_fwd_tile1(const double* __restrict__ src, AxisView sv,
                                                     double* __restrict__ dst, AxisView dv, int h,
                                                     FwdTaps<L> tp) {
@@ -113,7 +140,7 @@ __global__ __launch_bounds__(NT) void wpt_fwd_tile1(const double* __restrict__ s
   load_window<1, NT, (M0 + NT - 1) / NT>(lds, s, M0, true, 0, 1,
                                           [&](int e) { return (int64_t)((base + e) & msk); });
   dma_fence_barrier();
-  Wpt1FwdLevel<L, NT, T, K, FMA, 1>::run(tp, lds, h, t, dst + view_base(dv, o));
+  Wpt1FwdLevel<L, NT, T, K, FMA, 1, ILV>::run(tp, lds, h, t, dst + view_base(dv, o));
 }
 
 // ---------------------------------------------------------------- reverse
@@ -126,7 +153,35 @@ struct Wpt1RevGeo {
   static constexpr int lds_doubles() { return (1 << K) * len(K) + 4; }
 };
 
-template <int L, int NT, int T, int K, bool FMA, int l>
+// Couple (pairs m, m+1) of rev_pair with the term loop shared: A/D point at
+// a[m], d[m]; the four sums keep rev_pair's per-output order (q descending),
+// and are materialised after every term so the compiler cannot schedule the
+// four dependent add chains one after the other (it does for two rev_pair
+// calls: each add then waits on its predecessor).  Compiled-in L only.
+template <int L, bool FMA>
+__device__ __forceinline__ void rev_couple_ilv(const RevTaps<L>& tp, const double* A,
+                                               const double* D, double& e0, double& o0,
+                                               double& e1, double& o1) {
+  constexpr int QE = (L + 1) / 2, QO = L / 2;
+  double se0 = 0.0, so0 = 0.0, se1 = 0.0, so1 = 0.0;
+#pragma unroll
+  for (int q = QE - 1; q >= 0; --q) {
+    const double a0 = A[-q], d0 = D[-q], a1 = A[1 - q], d1 = D[1 - q];
+    se0 += mac<FMA>(a0 * FB<L>::lor(tp, 2 * q), d0, FB<L>::hir(tp, 2 * q));
+    se1 += mac<FMA>(a1 * FB<L>::lor(tp, 2 * q), d1, FB<L>::hir(tp, 2 * q));
+    if (q < QO) {
+      so0 += mac<FMA>(a0 * FB<L>::lor(tp, 2 * q + 1), d0, FB<L>::hir(tp, 2 * q + 1));
+      so1 += mac<FMA>(a1 * FB<L>::lor(tp, 2 * q + 1), d1, FB<L>::hir(tp, 2 * q + 1));
+    }
+    asm volatile("" : "+v"(se0), "+v"(so0), "+v"(se1), "+v"(so1));
+  }
+  e0 = se0;
+  o0 = so0;
+  e1 = se1;
+  o1 = so1;
+}
+
+template <int L, int NT, int T, int K, bool FMA, int l, bool ILV = false>
 struct Wpt1RevLevel {
   // lds: 2^l packet windows of len(l) (stride len(l)); produces 2^(l-1)
   // windows of len(l-1) (level 1: the T outputs, to y).  Each lane computes
@@ -174,8 +229,12 @@ struct Wpt1RevLevel {
         }
         // pair ml: a[li - q] = av[(Q-1) + sh - q]; pair ml+1: one further
         double x0e, x0o, x1e, x1o;
-        rev_pair<L, FMA>(tp, av + (Q - 1) + sh, dv + (Q - 1) + sh, 1, x0e, x0o);
-        rev_pair<L, FMA>(tp, av + Q + sh, dv + Q + sh, 1, x1e, x1o);
+        if constexpr (ILV) {
+          rev_couple_ilv<L, FMA>(tp, av + (Q - 1) + sh, dv + (Q - 1) + sh, x0e, x0o, x1e, x1o);
+        } else {
+          rev_pair<L, FMA>(tp, av + (Q - 1) + sh, dv + (Q - 1) + sh, 1, x0e, x0o);
+          rev_pair<L, FMA>(tp, av + Q + sh, dv + Q + sh, 1, x1e, x1o);
+        }
         asm volatile("" : "+v"(x0e), "+v"(x0o), "+v"(x1e), "+v"(x1o) :: "memory");  // slot boundary
         const int mg = pbase + ml;
         const bool w0 = !(head_tile && mg >= 0 && mg < Q - 1);
@@ -221,14 +280,14 @@ struct Wpt1RevLevel {
       }
       if (hs >= 0) *reinterpret_cast<double2*>(lds + hs * lo_ + 2 * hml) = make_double2(hxe, hxo);
       lds_barrier();
-      Wpt1RevLevel<L, NT, T, K, FMA, l - 1>::run(tp, lds, t, y);
+      Wpt1RevLevel<L, NT, T, K, FMA, l - 1, ILV>::run(tp, lds, t, y);
     }
   }
 };
 
 // Grid: rows * (h / T) blocks; h = output packet size of the pass; input
 // row o holds 2^K packets of h/2^K (view sv), output row o (view dv).
-template <int L, int NT, int T, int K, bool FMA>
+template <int L, int NT, int T, int K, bool FMA, bool ILV = false>
 __global__ __launch_bounds__(NT) void wpt_rev_tile1(const double* __restrict__ src, AxisView sv,
                                                     double* __restrict__ dst, AxisView dv, int h,
                                                     RevTaps<L> tp) {
@@ -252,7 +311,7 @@ __global__ __launch_bounds__(NT) void wpt_rev_tile1(const double* __restrict__ s
         return (int64_t)w * hp + ((BK + k) & pm);
       });
   dma_fence_barrier();
-  Wpt1RevLevel<L, NT, T, K, FMA, K>::run(tp, lds, t, dst + view_base(dv, o));
+  Wpt1RevLevel<L, NT, T, K, FMA, K, ILV>::run(tp, lds, t, dst + view_base(dv, o));
 }
 
 }  // namespace jwv
