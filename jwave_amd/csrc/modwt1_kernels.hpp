@@ -635,12 +635,15 @@ struct ModInv1Level {
     }
     lds_barrier();
     if constexpr (j == J0) {
+      const bool dfast = t0 + T <= N && (((uintptr_t)(dst + t0)) & 15) == 0;
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const int k = tid + r * NT;
         const int p = 2 * k;
         if (r * NT * 2 < T && p < T) {
-          if (t0 + p + 1 < N && p + 1 < T) {
+          if (dfast) {
+            mod_store2(dst + t0, p, vv[r].x, vv[r].y);
+          } else if (t0 + p + 1 < N && p + 1 < T) {
             *reinterpret_cast<double2*>(dst + t0 + p) = vv[r];
           } else {
             if (t0 + p < N) dst[t0 + p] = vv[r].x;
@@ -762,6 +765,8 @@ struct ModInv1Level {
       asm volatile("" ::: "memory");  // slot fence
     }
     lds_barrier();
+    // final level, whole tile inside the signal, 16-B aligned output: buffer stores
+    const bool dfast = j == J0 && t0 + T <= N && (((uintptr_t)(dst + t0)) & 15) == 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int t = tid + r * NT;
@@ -773,7 +778,9 @@ struct ModInv1Level {
         if constexpr (j == J0) {
           const int p = 2 * s;
           if (ok && p < T) {
-            if (t0 + p + 1 < N && p + 1 < T) {
+            if (dfast) {
+              mod_store2(dst + t0, p, vv[r][m].x, vv[r][m].y);
+            } else if (t0 + p + 1 < N && p + 1 < T) {
               *reinterpret_cast<double2*>(dst + t0 + p) = vv[r][m];
             } else if (t0 + p < N) {
               dst[t0 + p] = vv[r][m].x;
