@@ -32,15 +32,16 @@ hipError_t prep1(Kern kernel, size_t lds) {
 }
 
 // env JWV_FWD1CP (default 1): 0 = one pair per lane in the full-length
-// forward pass (conflict-free 16-B LDS reads) instead of couples
-bool fwd1_couples() {
-  static const bool v = [] {
+// forward pass (conflict-free 16-B LDS reads) instead of couples; 2 = couples
+// with the four sums interleaved (fwd_couple_ilv)
+int fwd1_couples() {
+  static const int v = [] {
     const char* e = std::getenv("JWV_FWD1CP");
-    return e ? std::atoi(e) != 0 : true;
+    return e ? std::atoi(e) : 1;
   }();
   return v;
 }
-template <int L, int NT, int T, int K, bool CP = true>
+template <int L, int NT, int T, int K, int CP = 1>
 hipError_t fwd1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
   auto k = fwt_fwd_tile1<L, NT, T, K, kFMA, CP>;
   const size_t lds = (size_t)Fwd1Geo<L, T, K>::lds_doubles() * sizeof(double);
@@ -70,7 +71,8 @@ hipError_t fwd1_l(const Bank& b, const TileArgs& a, hipStream_t s) {
     case 4: return fwd1_k<L, NT, T, 4>(b, a, s);
     case 5: return fwd1_k<L, NT, T, 5>(b, a, s);
     case 6:
-      if (L <= 8 && !fwd1_couples()) return fwd1_k<L, NT, T, 6, false>(b, a, s);
+      if (L <= 8 && fwd1_couples() == 0) return fwd1_k<L, NT, T, 6, 0>(b, a, s);
+      if (L <= 8 && fwd1_couples() == 2) return fwd1_k<L, NT, T, 6, 2>(b, a, s);
       return fwd1_k<L, NT, T, 6>(b, a, s);
     // deep passes (latency-bound, few blocks): 512 threads halve the pair
     // slots of the wide levels (config 2: 0.6 us per call)

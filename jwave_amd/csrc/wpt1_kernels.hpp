@@ -32,29 +32,6 @@ struct Wpt1FwdGeo {
   static_assert((L & 1) == 0 && ((T >> K) & 1) == 0, "even windows");
 };
 
-// Couple (pairs i, i+1) of fwd_pair with the tap loop shared: x[j] = window
-// sample 2i + j; the four sums keep fwd_pair's per-output order (j ascending
-// from +0.0) and are materialised after every tap, so the four dependent add
-// chains stay interleaved (the compiler otherwise runs two, each add waiting on
-// the multiply it consumes and on the previous add).
-template <int L, bool FMA>
-__device__ __forceinline__ void fwd_couple_ilv(const FwdTaps<L>& tp, const double* x, double& a0,
-                                               double& d0, double& a1, double& d1) {
-  double sa0 = 0.0, sd0 = 0.0, sa1 = 0.0, sd1 = 0.0;
-#pragma unroll
-  for (int j = 0; j < L; ++j) {
-    sa0 = mac<FMA>(sa0, x[j], FB<L>::lo(tp, j));
-    sd0 = mac<FMA>(sd0, x[j], FB<L>::hi(tp, j));
-    sa1 = mac<FMA>(sa1, x[j + 2], FB<L>::lo(tp, j));
-    sd1 = mac<FMA>(sd1, x[j + 2], FB<L>::hi(tp, j));
-    asm volatile("" : "+v"(sa0), "+v"(sd0), "+v"(sa1), "+v"(sd1));
-  }
-  a0 = sa0;
-  d0 = sd0;
-  a1 = sa1;
-  d1 = sd1;
-}
-
 template <int L, int NT, int T, int K, bool FMA, int l, bool ILV = false>
 struct Wpt1FwdLevel {
   // lds: 2^(l-1) input sub-windows of m(l-1) samples (stride m(l-1)).
