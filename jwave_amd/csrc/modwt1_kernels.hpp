@@ -94,6 +94,7 @@ struct ModFwd1Geo {
     return kPad + e0(j) + 2 * nb * M * h;
   }
   static constexpr int lds_doubles(int M) {
+    M %= 1000;
     int b = lds_doubles();
     if (M % 100 > 1)
       for (int j = J0; j <= J1; ++j) {
@@ -114,7 +115,8 @@ template <int L, int NT, int T, int J0, int J1, bool FMA, int j, bool P2, int M 
 struct ModFwd1Level {
   static constexpr int kPad = ModFwd1Geo<L, T, J0, J1>::kPad;
   // M = m + 100*jr: run form with m pairs per lane on levels j >= jr
-  static constexpr int kM = M % 100, kJR = M / 100;
+  static constexpr int kM = M % 100, kJR = (M / 100) % 10;
+  static constexpr bool kILV = M >= 1000;  // all 4*kM sums interleaved per tap
   static constexpr bool kRun = kM > 1 && j >= kJR;
   __device__ __forceinline__ static void run_p2(const ModwtTaps<L>& tp, double* lds,
                                                 double* __restrict__ wout, int64_t ldw,
@@ -219,6 +221,7 @@ struct ModFwd1Level {
     const int tid = opaque_tid();
     double* __restrict__ wrow = wout + (int64_t)(j - 1) * ldw + (t0 - G::S);
     const bool w16 = (((uintptr_t)wrow + 8 * e0) & 15) == 0;
+    const bool wfast = w16 && t0 + T <= N;  // buffer stores (see run_p2)
     double* const B = lds + kPad + e0;  // slot 0 of this level, 16-B aligned
     double2 vv[R][kM];
 #pragma unroll
@@ -238,20 +241,41 @@ struct ModFwd1Level {
         v[2 * k + 1] = u.y;
       }
       double sw[kM][2], sv[kM][2];
+      if constexpr (kILV) {
 #pragma unroll
-      for (int m = 0; m < kM; ++m) {
+        for (int m = 0; m < kM; ++m) sw[m][0] = sw[m][1] = sv[m][0] = sv[m][1] = 0.0;
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          double a = 0.0, c = 0.0;
+        for (int l = 0; l < L; ++l) {
 #pragma unroll
-          for (int l = 0; l < L; ++l) {
-            const double x = st == 1 ? v[2 * m + q - l + L] : v[2 * (m - l + L - 1) + q];
-            a = mac<FMA>(a, x, tp.h[l]);
-            c = mac<FMA>(c, x, tp.g[l]);
+          for (int m = 0; m < kM; ++m)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              const double x = st == 1 ? v[2 * m + q - l + L] : v[2 * (m - l + L - 1) + q];
+              sw[m][q] = mac<FMA>(sw[m][q], x, tp.h[l]);
+              sv[m][q] = mac<FMA>(sv[m][q], x, tp.g[l]);
+            }
+#pragma unroll
+          for (int m = 0; m < kM; ++m) {
+            pin2(sw[m][0], sw[m][1]);
+            pin2(sv[m][0], sv[m][1]);
           }
-          pin2(a, c);
-          sw[m][q] = a;
-          sv[m][q] = c;
+        }
+      } else {
+#pragma unroll
+        for (int m = 0; m < kM; ++m) {
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            double a = 0.0, c = 0.0;
+#pragma unroll
+            for (int l = 0; l < L; ++l) {
+              const double x = st == 1 ? v[2 * m + q - l + L] : v[2 * (m - l + L - 1) + q];
+              a = mac<FMA>(a, x, tp.h[l]);
+              c = mac<FMA>(c, x, tp.g[l]);
+            }
+            pin2(a, c);
+            sw[m][q] = a;
+            sv[m][q] = c;
+          }
         }
       }
 #pragma unroll
@@ -261,7 +285,9 @@ struct ModFwd1Level {
         const int ee = e0 + 2 * s;  // S has e0's parity: a pair is all halo or all own
         if ((full || t < NTASK) && s < NS && ee >= G::S) {
           const int64_t g = t0 + (ee - G::S);
-          if (w16 && g + 1 < N) {
+          if (wfast) {
+            mod_store2(wrow, ee, sw[m][0], sw[m][1]);
+          } else if (w16 && g + 1 < N) {
             *reinterpret_cast<double2*>(wrow + ee) = make_double2(sw[m][0], sw[m][1]);
           } else {
             if (g < N) wrow[ee] = sw[m][0];
