@@ -46,12 +46,24 @@ bool wpt_ilv() {
   }();
   return v;
 }
-template <int L, int K, bool ILV = false>
+// env JWV_WPT_NODMA=1 (diagnostic): the config-4 reverse tile loads its
+// windows through registers instead of LDS-DMA
+bool wpt_nodma() {
+  static const bool v = [] {
+    const char* e = std::getenv("JWV_WPT_NODMA");
+    return e && std::atoi(e) != 0;
+  }();
+  return v;
+}
+template <int L, int K, bool ILV = false, bool DMA = true>
 hipError_t wrev1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
   if constexpr (!ILV && L >= 8) {
     if (wpt_ilv()) return wrev1_k<L, K, true>(b, a, s);
   }
-  auto k = wpt_rev_tile1<L, 256, kWptT, K, kFMA, ILV>;
+  if constexpr (ILV && DMA && L == 16 && K == 6) {
+    if (wpt_nodma()) return wrev1_k<L, K, true, false>(b, a, s);
+  }
+  auto k = wpt_rev_tile1<L, 256, kWptT, K, kFMA, ILV, DMA>;
   const size_t lds = (size_t)Wpt1RevGeo<L, kWptT, K>::lds_doubles() * sizeof(double);
   if (hipError_t e = prep1(k, lds)) return e;
   RevTaps<L> tp;

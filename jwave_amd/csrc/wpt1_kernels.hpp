@@ -264,7 +264,9 @@ struct Wpt1RevLevel {
 
 // Grid: rows * (h / T) blocks; h = output packet size of the pass; input
 // row o holds 2^K packets of h/2^K (view sv), output row o (view dv).
-template <int L, int NT, int T, int K, bool FMA, bool ILV = false>
+// DMA = false: the windows through registers (diagnostic A/B of the LDS-DMA
+// load's share of the LDS counters)
+template <int L, int NT, int T, int K, bool FMA, bool ILV = false, bool DMA = true>
 __global__ __launch_bounds__(NT) void wpt_rev_tile1(const double* __restrict__ src, AxisView sv,
                                                     double* __restrict__ dst, AxisView dv, int h,
                                                     RevTaps<L> tp) {
@@ -283,7 +285,7 @@ __global__ __launch_bounds__(NT) void wpt_rev_tile1(const double* __restrict__ s
   const int BK = t * (T >> K) - G::c(K);
   // all 2^K packet windows in one burst: window w -> lds[w * LK ..)
   load_window<1, NT, (NW * LK + NT - 1) / NT>(
-      lds, s, NW * LK, true, 0, 1, [&](int e) {
+      lds, s, NW * LK, DMA, 0, 1, [&](int e) {
         const int w = e / LK, k = e - w * LK;
         return (int64_t)w * hp + ((BK + k) & pm);
       });
