@@ -174,6 +174,9 @@ hipError_t inv_k(const Bank& b, const ModwtArgs& a, hipStream_t s) {
       case 2: return inv_kp<L, J1, true, 256, 1024>(b, a, s);
       case 3: return inv_kp<L, J1, true, 1024, 4096>(b, a, s);
       case 4: return inv_kp<L, J1, true, 256, 2048>(b, a, s);
+      case 5: return inv_kp<L, J1, true, 1024, 4096, 303>(b, a, s);
+      case 6: return inv_kp<L, J1, true, 512, 1536, 303>(b, a, s);
+      case 7: return inv_kp<L, J1, true, 256, 1024, 303>(b, a, s);
       default:
         if (p2_bits() & 2) {
           if (pf_env() & 2) {
