@@ -87,11 +87,31 @@ bool wpt_ilvf() {
   }();
   return v;
 }
+// env JWV_WPT_TRI (default 0): the 8192 forward tiles (L = 16) in the triple
+// form (Wpt1FwdLevel3: odd 48-B lane stride, conflict-free reads)
+bool wpt_tri() {
+  static const bool v = [] {
+    const char* e = std::getenv("JWV_WPT_TRI");
+    return e && std::atoi(e) != 0;
+  }();
+  return v;
+}
 template <int L, bool FWD, bool ILV = false>
 hipError_t wpt8k(const Bank& b, const TileArgs& a, hipStream_t s) {
   constexpr int TT = 8192, K = 6;
   const dim3 grid((unsigned)(a.nouter * (a.h / TT)));
   if constexpr (FWD) {
+    if constexpr (!ILV && L == 16) {
+      if (wpt_tri()) {  // triple form (wpt_fwd_tile1t)
+        auto k = wpt_fwd_tile1t<L, 512, TT, K, kFMA>;
+        const size_t lds = (size_t)Wpt1FwdGeo<L, TT, K>::lds_doubles() * sizeof(double);
+        if (hipError_t e = prep1(k, lds)) return e;
+        FwdTaps<L> tp;
+        for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
+        hipLaunchKernelGGL(k, grid, dim3(512), lds, s, a.src, a.sv, a.dst, a.dv, a.h, tp);
+        return hipGetLastError();
+      }
+    }
     if constexpr (!ILV && L >= 8)
       if (wpt_ilvf()) return wpt8k<L, true, true>(b, a, s);
     auto k = wpt_fwd_tile1<L, 512, TT, K, kFMA, ILV>;

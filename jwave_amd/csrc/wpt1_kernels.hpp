@@ -28,7 +28,8 @@ namespace jwv {
 template <int L, int T, int K>
 struct Wpt1FwdGeo {
   static constexpr int m(int l) { return (T >> l) + (L - 2) * ((1 << (K - l)) - 1); }
-  static constexpr int lds_doubles() { return m(0) + 2; }
+  // + 6: the triple form reads up to 3 samples past a sub-window
+  static constexpr int lds_doubles() { return m(0) + 6; }
   static_assert((L & 1) == 0 && ((T >> K) & 1) == 0, "even windows");
 };
 
@@ -118,6 +119,106 @@ __global__ __launch_bounds__(NT) void wpt_fwd_tile1(const double* __restrict__ s
                                           [&](int e) { return (int64_t)((base + e) & msk); });
   dma_fence_barrier();
   Wpt1FwdLevel<L, NT, T, K, FMA, 1, ILV>::run(tp, lds, h, t, dst + view_base(dv, o));
+}
+
+// Triple form of Wpt1FwdLevel: a lane computes three adjacent pairs (i0,
+// i0+1, i0+2) of one sub-window from L+4 window samples read as (L+4)/2
+// 16-B LDS reads.  Lanes sit 48 B (3 slots) apart, an odd slot stride, so a
+// 16-lane ds_read_b128 group covers 16 distinct slots mod 16 (the couples'
+// 32-B stride covers 8: 2-way conflicts on every read), and each pair costs
+// 10/3 reads instead of 9/2.  The write-back (three 8-B stores per operand at
+// a 24-B lane stride) is conflict-free as well.  Same per-output order
+// (fwd_pair), so EXACT results are unchanged.
+template <int L, int NT, int T, int K, bool FMA, int l>
+struct Wpt1FwdLevel3 {
+  __device__ __forceinline__ static void run(const FwdTaps<L>& tp, double* lds, int h, int t,
+                                             double* __restrict__ y) {
+    using G = Wpt1FwdGeo<L, T, K>;
+    constexpr int mi = G::m(l - 1), mo = G::m(l);
+    constexpr int N3 = (mo + 2) / 3;                // triples per sub-window
+    constexpr int NC = (1 << (l - 1)) * N3;         // triples of the level
+    constexpr int R = (NC + NT - 1) / NT;
+    const int tid = opaque_tid();
+    double ra[R][3], rd[R][3];
+    int wo[R];  // write-back offset (2s)*mo + i0
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int q = tid + r * NT;
+      if ((r + 1) * NT <= NC || q < NC) {
+        const int s = q / N3, i0 = 3 * (q % N3);
+        wo[r] = (2 * s) * mo + i0;
+        const double* in = lds + s * mi + 2 * i0;  // 16-B aligned: mi even, 2*i0 = 6u
+        double x[L + 4];
+#pragma unroll
+        for (int j = 0; j < L + 4; j += 2) {
+          const double2 v = *reinterpret_cast<const double2*>(in + j);
+          x[j] = v.x;
+          x[j + 1] = v.y;
+        }
+        double a[3], d[3];
+#pragma unroll
+        for (int m = 0; m < 3; ++m)
+          fwd_pair<L, FMA>(tp, [&](int j) { return x[j + 2 * m]; }, a[m], d[m]);
+        asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(d[0]), "+v"(d[1]), "+v"(d[2])
+                     :: "memory");  // slot boundary
+        if constexpr (l == K) {
+          const int hp = h >> K;
+          double* pa = y + (int64_t)(2 * s) * hp + t * (T >> K) + i0;
+#pragma unroll
+          for (int m = 0; m < 3; ++m)
+            if (i0 + m < mo) {
+              pa[m] = a[m];
+              pa[hp + m] = d[m];
+            }
+        } else {
+#pragma unroll
+          for (int m = 0; m < 3; ++m) {
+            ra[r][m] = a[m];
+            rd[r][m] = d[m];
+          }
+        }
+      }
+    }
+    if constexpr (l < K) {
+      lds_barrier();
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int q = tid + r * NT;
+        if ((r + 1) * NT <= NC || q < NC) {
+          const int i0 = wo[r] % mo;  // == 3 * (q % N3): (2s)*mo is a multiple of mo
+#pragma unroll
+          for (int m = 0; m < 3; ++m)
+            if (i0 + m < mo) {
+              lds[wo[r] + m] = ra[r][m];
+              lds[wo[r] + mo + m] = rd[r][m];
+            }
+        }
+      }
+      lds_barrier();
+      Wpt1FwdLevel3<L, NT, T, K, FMA, l + 1>::run(tp, lds, h, t, y);
+    }
+  }
+};
+
+template <int L, int NT, int T, int K, bool FMA>
+__global__ __launch_bounds__(NT) void wpt_fwd_tile1t(const double* __restrict__ src, AxisView sv,
+                                                     double* __restrict__ dst, AxisView dv, int h,
+                                                     FwdTaps<L> tp) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  using G = Wpt1FwdGeo<L, T, K>;
+  constexpr int M0 = G::m(0);
+  const int ntile = h / T;
+  const int nblk = gridDim.x;
+  int b = blockIdx.x;
+  if ((nblk & 7) == 0) b = (b & 7) * (nblk >> 3) + (b >> 3);
+  const int t = b % ntile;
+  const int64_t o = b / ntile;
+  const double* s = src + view_base(sv, o);
+  const int msk = h - 1, base = t * T;
+  load_window<1, NT, (M0 + NT - 1) / NT>(lds, s, M0, true, 0, 1,
+                                          [&](int e) { return (int64_t)((base + e) & msk); });
+  dma_fence_barrier();
+  Wpt1FwdLevel3<L, NT, T, K, FMA, 1>::run(tp, lds, h, t, dst + view_base(dv, o));
 }
 
 // ---------------------------------------------------------------- reverse
