@@ -259,7 +259,7 @@ __device__ __forceinline__ void rev_couple_ilv(const RevTaps<L>& tp, const doubl
   o1 = so1;
 }
 
-template <int L, int NT, int T, int K, bool FMA, int l, bool ILV = false>
+template <int L, int NT, int T, int K, bool FMA, int l, bool ILV = false, int DG = 0>
 struct Wpt1RevLevel {
   // lds: 2^l packet windows of len(l) (stride len(l)); produces 2^(l-1)
   // windows of len(l-1) (level 1: the T outputs, to y).  Each lane computes
@@ -351,14 +351,21 @@ struct Wpt1RevLevel {
       for (int r = 0; r < R; ++r) {
         const int k = tid + r * NT;
         if ((r + 1) * NT <= NC || k < NC) {
-          double* ob = lds + (wo[r] >> 2);
-          if (wo[r] & 1) *reinterpret_cast<double2*>(ob) = make_double2(rx[r].x, rx[r].y);
-          if (wo[r] & 2) *reinterpret_cast<double2*>(ob + 2) = make_double2(rx[r].z, rx[r].w);
+          if constexpr (DG == 1) {
+            // diagnostic (wrong results): the same two 16-B stores per couple
+            // at a 16-B lane stride into the first 4*NT doubles
+            *reinterpret_cast<double2*>(lds + 2 * tid) = make_double2(rx[r].x, rx[r].y);
+            *reinterpret_cast<double2*>(lds + 2 * (tid + NT)) = make_double2(rx[r].z, rx[r].w);
+          } else {
+            double* ob = lds + (wo[r] >> 2);
+            if (wo[r] & 1) *reinterpret_cast<double2*>(ob) = make_double2(rx[r].x, rx[r].y);
+            if (wo[r] & 2) *reinterpret_cast<double2*>(ob + 2) = make_double2(rx[r].z, rx[r].w);
+          }
         }
       }
       if (hs >= 0) *reinterpret_cast<double2*>(lds + hs * lo_ + 2 * hml) = make_double2(hxe, hxo);
       lds_barrier();
-      Wpt1RevLevel<L, NT, T, K, FMA, l - 1, ILV>::run(tp, lds, t, y);
+      Wpt1RevLevel<L, NT, T, K, FMA, l - 1, ILV, DG>::run(tp, lds, t, y);
     }
   }
 };
@@ -367,7 +374,7 @@ struct Wpt1RevLevel {
 // row o holds 2^K packets of h/2^K (view sv), output row o (view dv).
 // DMA = false: the windows through registers (diagnostic A/B of the LDS-DMA
 // load's share of the LDS counters)
-template <int L, int NT, int T, int K, bool FMA, bool ILV = false, bool DMA = true>
+template <int L, int NT, int T, int K, bool FMA, bool ILV = false, bool DMA = true, int DG = 0>
 __global__ __launch_bounds__(NT) void wpt_rev_tile1(const double* __restrict__ src, AxisView sv,
                                                     double* __restrict__ dst, AxisView dv, int h,
                                                     RevTaps<L> tp) {
@@ -391,7 +398,7 @@ __global__ __launch_bounds__(NT) void wpt_rev_tile1(const double* __restrict__ s
         return (int64_t)w * hp + ((BK + k) & pm);
       });
   dma_fence_barrier();
-  Wpt1RevLevel<L, NT, T, K, FMA, K, ILV>::run(tp, lds, t, dst + view_base(dv, o));
+  Wpt1RevLevel<L, NT, T, K, FMA, K, ILV, DG>::run(tp, lds, t, dst + view_base(dv, o));
 }
 
 }  // namespace jwv
