@@ -1,0 +1,61 @@
+"""Host-side checks of the MODWT run-form lane mapping (modwt1_kernels.hpp, ModRun).
+
+A lane takes task t -> (block, residue) = (t // h, t % h) and computes the M
+output-pair slots s0 + m*h, s0 = block*M*h + residue, at level stride
+st = 2^(j-1) (h = st/2, h = 1 at st = 1).  These tests restate that mapping
+and check, without a GPU, the two properties the kernel relies on:
+  * the valid tasks of a level cover every output-pair slot exactly once;
+  * within each 16-lane ds_read_b128 lane group of a wave (the gfx950 LDS
+    bank model, MI355X_MICROARCH.md "LDS"), the lanes' first read slots are
+    distinct mod 16 for odd M (every later read of the run shifts all lanes
+    by the same amount), so the reads are conflict-free at every stride.
+"""
+import pytest
+
+# ds_read_b128 lane groups of a wave64 (MI355X_MICROARCH.md, LDS table)
+B128_GROUPS = [
+    list(range(0, 4)) + list(range(12, 16)) + list(range(20, 28)),
+    list(range(4, 12)) + list(range(16, 20)) + list(range(28, 32)),
+    list(range(32, 36)) + list(range(44, 48)) + list(range(52, 60)),
+    list(range(36, 44)) + list(range(48, 52)) + list(range(60, 64)),
+]
+
+
+def slot0(t, m, st):
+    h = st // 2 if st >= 2 else 1
+    return (t // h) * (m * h) + (t % h), h
+
+
+def n_tasks(ns, m, st):
+    h = st // 2 if st >= 2 else 1
+    nb = (ns + m * h - 1) // (m * h)
+    return nb * h
+
+
+@pytest.mark.parametrize("m", [3, 5])
+@pytest.mark.parametrize("j", range(1, 9))
+def test_run_tasks_cover_every_slot_once(m, j):
+    st = 1 << (j - 1)
+    for ns in (1, 7, 64, 1024, 1213, 1469):  # config-5 level sizes included
+        seen = []
+        for t in range(n_tasks(ns, m, st)):
+            s0, h = slot0(t, m, st)
+            seen += [s0 + k * h for k in range(m) if s0 + k * h < ns]
+        assert sorted(seen) == list(range(ns)), (m, j, ns)
+
+
+@pytest.mark.parametrize("m", [3, 5])
+@pytest.mark.parametrize("j", range(1, 9))
+def test_run_reads_conflict_free(m, j):
+    st = 1 << (j - 1)
+    for wave in range(4):  # any wave: task = 64*wave + lane
+        for grp in B128_GROUPS:
+            slots = [slot0(64 * wave + lane, m, st)[0] % 16 for lane in grp]
+            assert len(set(slots)) == 16, (m, j, wave, slots)
+
+
+def test_even_m_would_conflict():
+    """The reason M is odd: with M = 2 the small strides collide."""
+    grp = B128_GROUPS[0]
+    slots = [slot0(lane, 2, 2)[0] % 16 for lane in grp]
+    assert len(set(slots)) < 16
