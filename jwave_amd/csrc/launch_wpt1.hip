@@ -55,6 +55,15 @@ bool wpt_nodma() {
   }();
   return v;
 }
+// env JWV_WPT_PAD=1: the config-4 reverse tile with padded window strides
+// (conflict-free reads across window boundaries by the bank model)
+bool wpt_pad() {
+  static const bool v = [] {
+    const char* e = std::getenv("JWV_WPT_PAD");
+    return e && std::atoi(e) != 0;
+  }();
+  return v;
+}
 // env JWV_WPT_DIAGW=1 (diagnostic only, WRONG results): the config-4 reverse
 // tile's LDS write-back at a 16-B lane stride (its LDS-conflict share)
 bool wpt_diagw() {
@@ -71,6 +80,16 @@ hipError_t wrev1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
   }
   if constexpr (ILV && DMA && L == 16 && K == 6) {
     if (wpt_nodma()) return wrev1_k<L, K, true, false>(b, a, s);
+    if (wpt_pad()) {  // padded window strides (Wpt1RevGeo::stride)
+      auto k = wpt_rev_tile1<L, 256, kWptT, K, kFMA, true, true, 0, true>;
+      const size_t lds = (size_t)Wpt1RevGeo<L, kWptT, K>::lds_doubles(true) * sizeof(double);
+      if (hipError_t e = prep1(k, lds)) return e;
+      RevTaps<L> tp;
+      for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
+      hipLaunchKernelGGL(k, dim3((unsigned)(a.nouter * (a.h / kWptT))), dim3(256), lds, s, a.src,
+                         a.sv, a.dst, a.dv, a.h, tp);
+      return hipGetLastError();
+    }
     if (wpt_diagw()) {  // diagnostic: conflict-free write-back, wrong results
       auto k = wpt_rev_tile1<L, 256, kWptT, K, kFMA, true, true, 1>;
       const size_t lds = (size_t)Wpt1RevGeo<L, kWptT, K>::lds_doubles() * sizeof(double);
