@@ -3,15 +3,19 @@
  *
  * Arrays cross the boundary by copy, never by pinning the Java heap: inputs
  * are copied with GetDoubleArrayRegion into page-locked staging memory of the
- * calling thread (jwv_host_alloc), the host-pointer C ABI entry DMAs that
- * buffer straight to the GPU, computes, DMAs the result into a second
- * page-locked buffer, and SetDoubleArrayRegion copies it into the Java
- * output.  No JNI critical region is held while the GPU works, so the
+ * calling thread (jwv_host_alloc; arrays above 64 MiB into pageable memory
+ * of the call), the host-pointer C ABI entry DMAs that buffer to the GPU,
+ * computes, DMAs the result into a second staging buffer, and
+ * SetDoubleArrayRegion copies it into the Java output.  Bad arrays (too
+ * short), bad taps and allocation failures leave a Java exception pending
+ * (ArrayIndexOutOfBounds / IllegalArgument / OutOfMemoryError) and return
+ * STAGE_FAIL before any GPU work; other statuses go to HipNative.check.  No JNI critical region is held while the GPU works, so the
  * collector is never blocked by a transform (a ForkJoin pool of callers,
  * ParallelTransform.java:240-270, keeps running).  Taps are copied into
  * small local arrays.
  *
- * Build (needs a JDK; the development image has none — source only here):
+ * Build (needs a JDK; the development image has none: tests/jni compiles and
+ * runs this file against a JNI test double, tests/test_jni_shim.py):
  *   gcc -O2 -shared -fPIC -I$JAVA_HOME/include -I$JAVA_HOME/include/linux \
  *       -I../../include jwave_hip_jni.c -L../../jwave_amd/lib -ljwave_hip \
  *       -lpthread -Wl,-rpath,'$ORIGIN' -o libjwave_hip_jni.so
@@ -24,15 +28,26 @@
 #include "jwave_hip.h"
 
 #define CTX(h) ((jwv_ctx*)(intptr_t)(h))
-#define STAGE_FAIL (-100) /* a Java exception is pending (bad array length) or no staging */
+#define STAGE_FAIL (-100) /* a Java exception is pending: bad array, bad taps, no memory */
 
-/* Per-thread page-locked staging: two buffers (in, out), grown on demand,
- * freed when the thread exits. */
+/* Per-thread page-locked staging: two buffers (in, out) of at most
+ * STAGE_PIN_MAX bytes each, grown on demand and kept for the thread's next
+ * call, freed when the thread exits.  Larger arrays are staged in pageable
+ * memory allocated for the one call (the library's host entries then move
+ * them through their own pinned chunk ring), so a pool thread that once
+ * transformed a big matrix does not keep gigabytes pinned. */
+#define STAGE_PIN_MAX ((int64_t)64 << 20)
+
 typedef struct {
   jwv_ctx* ctx;
   void* p[2];
   int64_t bytes[2];
 } staging;
+
+typedef struct {
+  double* p;
+  int owned; /* 1: pageable, freed by buf_put */
+} buf_t;
 
 static pthread_key_t g_stage_key;
 static pthread_once_t g_stage_once = PTHREAD_ONCE_INIT;
@@ -45,33 +60,63 @@ static void stage_free(void* v) {
 }
 static void stage_key_init(void) { pthread_key_create(&g_stage_key, stage_free); }
 
-static double* stage_buf(jwv_ctx* ctx, int which, int64_t n) {
-  pthread_once(&g_stage_once, stage_key_init);
-  staging* s = (staging*)pthread_getspecific(g_stage_key);
-  if (!s) {
-    s = (staging*)calloc(1, sizeof(staging));
-    if (!s) return NULL;
-    s->ctx = ctx;
-    pthread_setspecific(g_stage_key, s);
-  }
-  const int64_t bytes = (n > 0 ? n : 1) * (int64_t)sizeof(double);
-  if (s->bytes[which] < bytes) {
-    if (s->p[which]) jwv_host_free(s->ctx, s->p[which]);
-    s->p[which] = NULL;
-    s->bytes[which] = 0;
-    s->ctx = ctx;
-    if (jwv_host_alloc(ctx, bytes, &s->p[which]) != JWV_OK) return NULL;
-    s->bytes[which] = bytes;
-  }
-  return (double*)s->p[which];
+static void throw_java(JNIEnv* env, const char* cls, const char* msg) {
+  jclass c = (*env)->FindClass(env, cls);
+  if (c) (*env)->ThrowNew(env, c, msg);
 }
 
-/* Java array -> staging buffer `which` (n doubles) */
-static double* stage_in(JNIEnv* env, jwv_ctx* ctx, int which, jdoubleArray a, int64_t n) {
-  double* d = stage_buf(ctx, which, n);
-  if (!d) return NULL;
-  if (n > 0) (*env)->GetDoubleArrayRegion(env, a, 0, (jsize)n, d);
-  return (*env)->ExceptionCheck(env) ? NULL : d;
+/* staging buffer `which` for n doubles; 0, or STAGE_FAIL with an
+ * OutOfMemoryError pending */
+static int buf_get(JNIEnv* env, jwv_ctx* ctx, int which, int64_t n, buf_t* b) {
+  const int64_t bytes = (n > 0 ? n : 1) * (int64_t)sizeof(double);
+  b->p = NULL;
+  b->owned = 0;
+  if (bytes > STAGE_PIN_MAX) {
+    b->p = (double*)malloc((size_t)bytes);
+    b->owned = 1;
+  } else {
+    pthread_once(&g_stage_once, stage_key_init);
+    staging* s = (staging*)pthread_getspecific(g_stage_key);
+    if (!s && (s = (staging*)calloc(1, sizeof(staging))) != NULL) {
+      s->ctx = ctx;
+      pthread_setspecific(g_stage_key, s);
+    }
+    if (s && s->bytes[which] < bytes) {
+      if (s->p[which]) jwv_host_free(s->ctx, s->p[which]);
+      s->p[which] = NULL;
+      s->bytes[which] = 0;
+      s->ctx = ctx;
+      if (jwv_host_alloc(ctx, bytes, &s->p[which]) == JWV_OK) s->bytes[which] = bytes;
+    }
+    if (s && s->bytes[which] >= bytes) b->p = (double*)s->p[which];
+  }
+  if (!b->p) {
+    throw_java(env, "java/lang/OutOfMemoryError", "jwave_hip_jni: no staging memory");
+    return STAGE_FAIL;
+  }
+  return 0;
+}
+static void buf_put(buf_t* b) {
+  if (b->owned) free(b->p);
+  b->p = NULL;
+}
+
+/* Java array a (n doubles read) -> staging buffer `which` */
+static int stage_in(JNIEnv* env, jwv_ctx* ctx, int which, jdoubleArray a, int64_t n, buf_t* b) {
+  if (buf_get(env, ctx, which, n, b)) return STAGE_FAIL;
+  if (n > 0) (*env)->GetDoubleArrayRegion(env, a, 0, (jsize)n, b->p);
+  if ((*env)->ExceptionCheck(env)) {
+    buf_put(b);
+    return STAGE_FAIL;
+  }
+  return 0;
+}
+/* the output array must hold n doubles: checked before any GPU work */
+static int out_fits(JNIEnv* env, jdoubleArray a, int64_t n) {
+  if ((int64_t)(*env)->GetArrayLength(env, a) >= n) return 1;
+  throw_java(env, "java/lang/ArrayIndexOutOfBoundsException",
+             "jwave_hip_jni: output array shorter than the transform");
+  return 0;
 }
 /* staging buffer -> Java array, only after a successful call */
 static int stage_out(JNIEnv* env, jdoubleArray a, const double* d, int64_t n, int rc) {
@@ -87,10 +132,14 @@ typedef struct {
   jwv_taps t;
 } taps_buf;
 
-/* taps: copied (L <= JWV_MAX_TAPS, checked again by the library) */
+/* taps: copied (1 <= L <= JWV_MAX_TAPS, else IllegalArgumentException) */
 static int taps_of(JNIEnv* env, taps_buf* b, jint L, jint tw, jdouble scale, jdoubleArray jlo,
                    jdoubleArray jhi, jdoubleArray jlor, jdoubleArray jhir) {
-  if (L < 1 || L > JWV_MAX_TAPS) return JWV_ERR_BAD_CALL;
+  if (L < 1 || L > JWV_MAX_TAPS) {
+    throw_java(env, "java/lang/IllegalArgumentException",
+               "jwave_hip_jni: filter length outside 1..64");
+    return STAGE_FAIL;
+  }
   (*env)->GetDoubleArrayRegion(env, jlo, 0, L, b->lo);
   (*env)->GetDoubleArrayRegion(env, jhi, 0, L, b->hi);
   (*env)->GetDoubleArrayRegion(env, jlor, 0, L, b->lor);
@@ -127,15 +176,24 @@ JNIEXPORT jstring JNICALL Java_jwave_amd_HipNative_lastError(JNIEnv* env, jclass
   }                                                                  \
   const jwv_taps* t = &B.t
 
-/* x (nx doubles) and y (ny doubles) staged; body sets rc from x, y */
-#define STAGED(NX, NY, BODY)                                         \
+/* jx (NX doubles) and jy (NY doubles) staged; BODY sets rc from x, y */
+#define STAGED(JX, NX, JY, NY, BODY)                                 \
   do {                                                               \
-    const double* x = stage_in(env, CTX(ctx), 0, jx, (NX));          \
-    double* y = stage_buf(CTX(ctx), 1, (NY));                        \
-    if (!x || !y) return STAGE_FAIL;                                 \
+    if (!out_fits(env, (JY), (NY))) return STAGE_FAIL;               \
+    buf_t bx_, by_;                                                  \
+    if (stage_in(env, CTX(ctx), 0, (JX), (NX), &bx_)) return STAGE_FAIL; \
+    if (buf_get(env, CTX(ctx), 1, (NY), &by_)) {                     \
+      buf_put(&bx_);                                                 \
+      return STAGE_FAIL;                                             \
+    }                                                                \
+    const double* x = bx_.p;                                         \
+    double* y = by_.p;                                               \
     int rc;                                                          \
     BODY;                                                            \
-    return stage_out(env, jy, y, (NY), rc);                          \
+    rc = stage_out(env, (JY), y, (NY), rc);                          \
+    buf_put(&bx_);                                                   \
+    buf_put(&by_);                                                   \
+    return rc;                                                       \
   } while (0)
 
 /* FastWaveletTransform / WaveletPacketTransform forward|reverse(double[], int) */
@@ -145,7 +203,7 @@ JNIEXPORT jint JNICALL Java_jwave_amd_HipNative_transform1d(
     jdoubleArray jlor, jdoubleArray jhir) {
   const int64_t n = (*env)->GetArrayLength(env, jx);
   TAPS(B);
-  STAGED(n, n, {
+  STAGED(jx, n, jy, n, {
     if (kind == 0)
       rc = fwd ? jwv_fwt_fwd_f64(x, y, n, level, t, CTX(ctx))
                : jwv_fwt_rev_f64(x, y, n, level, t, CTX(ctx));
@@ -162,7 +220,7 @@ JNIEXPORT jint JNICALL Java_jwave_amd_HipNative_transformBatch(
     jdoubleArray jhi, jdoubleArray jlor, jdoubleArray jhir) {
   const int64_t tot = (int64_t)batch * n;
   TAPS(B);
-  STAGED(tot, tot, {
+  STAGED(jx, tot, jy, tot, {
     if (kind == 0)
       rc = fwd ? jwv_fwt_fwd_batch_f64(x, y, batch, n, n, level, t, CTX(ctx))
                : jwv_fwt_rev_batch_f64(x, y, batch, n, n, level, t, CTX(ctx));
@@ -179,7 +237,7 @@ JNIEXPORT jint JNICALL Java_jwave_amd_HipNative_transform2d(
     jdoubleArray jhi, jdoubleArray jlor, jdoubleArray jhir) {
   const int64_t tot = (int64_t)rows * cols;
   TAPS(B);
-  STAGED(tot, tot, {
+  STAGED(jx, tot, jy, tot, {
     if (kind == 0)
       rc = fwd ? jwv_fwt2d_fwd_f64(x, y, rows, cols, lm, ln, t, CTX(ctx))
                : jwv_fwt2d_rev_f64(x, y, rows, cols, lm, ln, t, CTX(ctx));
@@ -196,7 +254,7 @@ JNIEXPORT jint JNICALL Java_jwave_amd_HipNative_transform3d(
     jdoubleArray jlo, jdoubleArray jhi, jdoubleArray jlor, jdoubleArray jhir) {
   const int64_t tot = (int64_t)p * q * r;
   TAPS(B);
-  STAGED(tot, tot, {
+  STAGED(jx, tot, jy, tot, {
     if (kind == 0)
       rc = fwd ? jwv_fwt3d_fwd_f64(x, y, p, q, r, lp, lq, lr, t, CTX(ctx))
                : jwv_fwt3d_rev_f64(x, y, p, q, r, lp, lq, lr, t, CTX(ctx));
@@ -214,16 +272,8 @@ JNIEXPORT jint JNICALL Java_jwave_amd_HipNative_modwt(
   const jdouble scale = 1.0;
   const int64_t nw = (int64_t)(J + 1) * n;
   TAPS(B);
-  if (fwd) {
-    const double* x = stage_in(env, CTX(ctx), 0, jx, n);
-    double* wv = stage_buf(CTX(ctx), 1, nw);
-    if (!x || !wv) return STAGE_FAIL;
-    return stage_out(env, jwv, wv, nw, jwv_modwt_fwd_f64(x, wv, n, J, t, CTX(ctx)));
-  }
-  const double* wv = stage_in(env, CTX(ctx), 0, jwv, nw);
-  double* x = stage_buf(CTX(ctx), 1, n);
-  if (!wv || !x) return STAGE_FAIL;
-  return stage_out(env, jx, x, n, jwv_modwt_inv_f64(wv, x, n, J, t, CTX(ctx)));
+  if (fwd) STAGED(jx, n, jwv, nw, { rc = jwv_modwt_fwd_f64(x, y, n, J, t, CTX(ctx)); });
+  STAGED(jwv, nw, jx, n, { rc = jwv_modwt_inv_f64(x, y, n, J, t, CTX(ctx)); });
 }
 
 /* AncientEgyptianDecomposition(FWT | WPT).forward|reverse(double[]) of any
@@ -234,7 +284,7 @@ JNIEXPORT jint JNICALL Java_jwave_amd_HipNative_aed(
     jdoubleArray jhir) {
   const int64_t n = (*env)->GetArrayLength(env, jx);
   TAPS(B);
-  STAGED(n, n, {
+  STAGED(jx, n, jy, n, {
     rc = fwd ? jwv_aed_fwd_f64(x, y, n, kind, t, CTX(ctx))
              : jwv_aed_rev_f64(x, y, n, kind, t, CTX(ctx));
   });
@@ -248,7 +298,6 @@ JNIEXPORT jint JNICALL Java_jwave_amd_HipNative_decompose(
     jdoubleArray jhir) {
   const int64_t n = (*env)->GetArrayLength(env, jx);
   const int64_t nm = (*env)->GetArrayLength(env, jmat);
-  jdoubleArray jy = jmat;
   TAPS(B);
-  STAGED(n, nm, { rc = jwv_decompose_f64(x, y, n, kind, t, CTX(ctx)); });
+  STAGED(jx, n, jmat, nm, { rc = jwv_decompose_f64(x, y, n, kind, t, CTX(ctx)); });
 }

@@ -189,7 +189,8 @@ class ModwtShard:
     that are dropped, and every kept output sums the same values in the same
     order as the unsharded transform, so kept results are bit-identical."""
 
-    def __init__(self, n_global, w, J, device, group=None, dtype=torch.float64):
+    def __init__(self, n_global, w, J, device, group=None):
+        dtype = torch.float64  # the C-ABI _ld entries address these as doubles
         W, rank = _world(group)
         counts = [shard_range(n_global, W, r)[1] for r in range(W)]
         self.H = H = modwt_halo(w.mother_wavelength, J)

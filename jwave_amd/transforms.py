@@ -295,17 +295,33 @@ def modwt_inverse(coeffs, wavelet, ctx=None):
                 (n, int(J), _TapsHolder.of(wavelet)))
 
 
+def _check_ld(name, c, x):
+    """The _ld entries address c by raw pointer and row stride (in doubles) and
+    x as n contiguous doubles: both must be float64 tensors on one device, x
+    contiguous, c with unit column stride."""
+    import torch
+    if not (_is_torch(x) and x.is_cuda and _is_torch(c) and c.is_cuda):
+        raise JWaveError("%s takes float64 device tensors" % name)
+    if c.dtype != torch.float64 or x.dtype != torch.float64:
+        raise JWaveError("%s takes float64 device tensors (got %s, %s)" % (name, c.dtype, x.dtype))
+    if c.device != x.device:
+        raise JWaveError("%s: c and x on different devices (%s, %s)" % (name, c.device, x.device))
+    if not x.is_contiguous():
+        raise JWaveError("%s: x must be contiguous" % name)
+    if c.dim() != 2 or c.stride(1) != 1:
+        raise JWaveError("%s: c must be a 2-D matrix with unit column stride" % name)
+
+
 def modwt_forward_ld(x, c, n, J, wavelet, ctx=None):
     """forwardMODWT of the device signal x[:n] into the rows of the device
     matrix c (row stride c.stride(0) >= n), columns [0, n)
     (jwv_modwt_fwd_ld_f64_dev)."""
-    if not (_is_torch(x) and x.is_cuda and _is_torch(c) and c.is_cuda):
-        raise JWaveError("modwt_forward_ld takes float64 device tensors")
-    if c.stride(1) != 1 or c.shape[0] != J + 1 or c.shape[1] < n or x.numel() < n:
+    _check_ld("modwt_forward_ld", c, x)
+    if c.shape[0] != J + 1 or c.shape[1] < n or x.numel() < n:
         raise JWaveError("modwt_forward_ld: c must be [J+1][>= n] with unit column stride")
     ctx = _ctx_for(ctx, x)
-    px, keep, _ = _prep(x, ctx)
-    ctx._check(L.lib().jwv_modwt_fwd_ld_f64_dev(px, ctypes.c_void_p(c.data_ptr()), c.stride(0),
+    ctx.set_stream(__import__("torch").cuda.current_stream(x.device).cuda_stream)
+    ctx._check(L.lib().jwv_modwt_fwd_ld_f64_dev(ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(c.data_ptr()), c.stride(0),
                                                 int(n), int(J), _TapsHolder.of(wavelet),
                                                 ctx.handle))
 
@@ -314,9 +330,8 @@ def modwt_inverse_ld(c, col0, n, x, wavelet, ctx=None):
     """inverseMODWT of the columns [col0, col0 + n) of the device matrix c
     ([J+1] rows at stride c.stride(0)) into the device vector x[:n]
     (jwv_modwt_inv_ld_f64_dev)."""
-    if not (_is_torch(x) and x.is_cuda and _is_torch(c) and c.is_cuda):
-        raise JWaveError("modwt_inverse_ld takes float64 device tensors")
-    if c.stride(1) != 1 or col0 + n > c.shape[1] or x.numel() < n:
+    _check_ld("modwt_inverse_ld", c, x)
+    if col0 < 0 or col0 + n > c.shape[1] or x.numel() < n:
         raise JWaveError("modwt_inverse_ld: columns out of range")
     ctx = _ctx_for(ctx, x)
     ctx.set_stream(__import__("torch").cuda.current_stream(x.device).cuda_stream)
