@@ -183,6 +183,16 @@ int jwv_fwt3d_fwd_f64_dev(const double* x, double* y, int64_t p, int64_t q, int6
                           int lvl_p, int lvl_q, int lvl_r, const jwv_taps* t, jwv_ctx* ctx);
 int jwv_fwt3d_rev_f64_dev(const double* y, double* x, int64_t p, int64_t q, int64_t r,
                           int lvl_p, int lvl_q, int lvl_r, const jwv_taps* t, jwv_ctx* ctx);
+/* ParallelTransform.reverse(double[][][], lvlP, lvlQ, lvlR)
+ * (ParallelTransform.java:183-216) in ONE call: the P axis first (lvlR,
+ * Space3DTransformTask :386-394), then each slice's 2-D reverse (columns
+ * lvlP, rows lvlQ).  BasicTransform.reverse (:602-659) runs the slices first,
+ * so the two orders round differently; ParallelTransform.forward equals
+ * BasicTransform.forward and uses jwv_fwt3d_fwd_f64. */
+int jwv_fwt3d_rev_pt_f64(const double* y, double* x, int64_t p, int64_t q, int64_t r, int lvl_p,
+                         int lvl_q, int lvl_r, const jwv_taps* t, jwv_ctx* ctx);
+int jwv_fwt3d_rev_pt_f64_dev(const double* y, double* x, int64_t p, int64_t q, int64_t r,
+                             int lvl_p, int lvl_q, int lvl_r, const jwv_taps* t, jwv_ctx* ctx);
 
 /* ---- CompressorMagnitude / denoise ---------------------------------------------
  * CompressorMagnitude(threshold).compress(double[])
@@ -254,6 +264,10 @@ int jwv_wpt3d_fwd_f64(const double* x, double* y, int64_t p, int64_t q, int64_t 
                       int lvl_q, int lvl_r, const jwv_taps* t, jwv_ctx* ctx);
 int jwv_wpt3d_rev_f64(const double* y, double* x, int64_t p, int64_t q, int64_t r, int lvl_p,
                       int lvl_q, int lvl_r, const jwv_taps* t, jwv_ctx* ctx);
+/* ParallelTransform(WaveletPacketTransform).reverse 3-D order (see
+ * jwv_fwt3d_rev_pt_f64) */
+int jwv_wpt3d_rev_pt_f64(const double* y, double* x, int64_t p, int64_t q, int64_t r, int lvl_p,
+                         int lvl_q, int lvl_r, const jwv_taps* t, jwv_ctx* ctx);
 
 /* ---- AncientEgyptianDecomposition / decompose ----------------------------------
  * transform: which BasicTransform is wrapped. */

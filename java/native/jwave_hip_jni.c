@@ -264,6 +264,20 @@ JNIEXPORT jint JNICALL Java_jwave_amd_HipNative_transform3d(
   });
 }
 
+/* ParallelTransform.reverse(double[][][], lvlP, lvlQ, lvlR) order: the P axis
+ * first, then the slices (ParallelTransform.java:183-216; jwv_*3d_rev_pt_f64) */
+JNIEXPORT jint JNICALL Java_jwave_amd_HipNative_transform3dPt(
+    JNIEnv* env, jclass cls, jlong ctx, jint kind, jdoubleArray jx, jdoubleArray jy, jint p,
+    jint q, jint r, jint lp, jint lq, jint lr, jint L, jint tw, jdouble scale, jdoubleArray jlo,
+    jdoubleArray jhi, jdoubleArray jlor, jdoubleArray jhir) {
+  const int64_t tot = (int64_t)p * q * r;
+  TAPS(B);
+  STAGED(jx, tot, jy, tot, {
+    rc = kind == 0 ? jwv_fwt3d_rev_pt_f64(x, y, p, q, r, lp, lq, lr, t, CTX(ctx))
+                   : jwv_wpt3d_rev_pt_f64(x, y, p, q, r, lp, lq, lr, t, CTX(ctx));
+  });
+}
+
 /* MODWTTransform.forwardMODWT(x, J) -> wv ; inverseMODWT(wv) -> x */
 JNIEXPORT jint JNICALL Java_jwave_amd_HipNative_modwt(
     JNIEnv* env, jclass cls, jlong ctx, jboolean fwd, jdoubleArray jx, jdoubleArray jwv, jint n,

@@ -11,7 +11,7 @@ import jwave.exceptions.JWaveException;
 import jwave.transforms.FastWaveletTransform;
 import jwave.transforms.wavelets.Wavelet;
 
-public class HipFastWaveletTransform extends FastWaveletTransform {
+public class HipFastWaveletTransform extends FastWaveletTransform implements HipTransform {
 
   protected final HipNative.Taps _taps;
   protected final int _kind;
@@ -68,68 +68,35 @@ public class HipFastWaveletTransform extends FastWaveletTransform {
   }
 
   /** The bank this transform sends to the GPU, or null (Java fallback). */
-  HipNative.Taps taps( ) { return _taps; }
+  @Override public HipNative.Taps taps( ) { return _taps; }
 
-  int kind( ) { return _kind; }
+  @Override public int kind( ) { return _kind; }
 
   @Override public double[ ][ ] forward( double[ ][ ] m, int lvlM, int lvlN )
       throws JWaveException {
     if( _taps == null || !HipNative.fitsArray( m.length, m.length == 0 ? 0 : m[ 0 ].length ) )
       return super.forward( m, lvlM, lvlN );
-    return run2d( true, m, lvlM, lvlN );
+    return HipNative.run2d( _kind, _taps, true, m, lvlM, lvlN );
   }
 
   @Override public double[ ][ ] reverse( double[ ][ ] m, int lvlM, int lvlN )
       throws JWaveException {
     if( _taps == null || !HipNative.fitsArray( m.length, m.length == 0 ? 0 : m[ 0 ].length ) )
       return super.reverse( m, lvlM, lvlN );
-    return run2d( false, m, lvlM, lvlN );
-  }
-
-  private double[ ][ ] run2d( boolean fwd, double[ ][ ] m, int lvlM, int lvlN )
-      throws JWaveException {
-    int rows = m.length, cols = rows == 0 ? 0 : m[ 0 ].length;
-    double[ ] x = HipNative.pack( m ), y = new double[ x.length ];
-    HipNative.Taps t = _taps;
-    HipNative.check( HipNative.transform2d( HipNative.ctx( ), _kind, fwd, x, y, rows, cols, lvlM,
-        lvlN, t.L, t.tw, t.scale, t.lo, t.hi, t.loR, t.hiR ) );
-    return HipNative.unpack( y, rows, cols );
+    return HipNative.run2d( _kind, _taps, false, m, lvlM, lvlN );
   }
 
   @Override public double[ ][ ][ ] forward( double[ ][ ][ ] s, int lvlP, int lvlQ, int lvlR )
       throws JWaveException {
-    if( _taps == null || !fits3d( s ) )
+    if( _taps == null || !HipNative.fits3d( s ) )
       return super.forward( s, lvlP, lvlQ, lvlR );
-    return run3d( true, s, lvlP, lvlQ, lvlR );
+    return HipNative.run3d( _kind, _taps, true, false, s, lvlP, lvlQ, lvlR );
   }
 
   @Override public double[ ][ ][ ] reverse( double[ ][ ][ ] s, int lvlP, int lvlQ, int lvlR )
       throws JWaveException {
-    if( _taps == null || !fits3d( s ) )
+    if( _taps == null || !HipNative.fits3d( s ) )
       return super.reverse( s, lvlP, lvlQ, lvlR );
-    return run3d( false, s, lvlP, lvlQ, lvlR );
-  }
-
-  private static boolean fits3d( double[ ][ ][ ] s ) {
-    long P = s.length, Q = P == 0 ? 0 : s[ 0 ].length, R = Q == 0 ? 0 : s[ 0 ][ 0 ].length;
-    return HipNative.fitsArray( P * Q, R );
-  }
-
-  private double[ ][ ][ ] run3d( boolean fwd, double[ ][ ][ ] s, int lp, int lq, int lr )
-      throws JWaveException {
-    int P = s.length, Q = P == 0 ? 0 : s[ 0 ].length, R = Q == 0 ? 0 : s[ 0 ][ 0 ].length;
-    double[ ] x = new double[ P * Q * R ];
-    for( int i = 0; i < P; i++ )
-      for( int j = 0; j < Q; j++ )
-        System.arraycopy( s[ i ][ j ], 0, x, ( i * Q + j ) * R, R );
-    double[ ] y = new double[ x.length ];
-    HipNative.Taps t = _taps;
-    HipNative.check( HipNative.transform3d( HipNative.ctx( ), _kind, fwd, x, y, P, Q, R, lp, lq,
-        lr, t.L, t.tw, t.scale, t.lo, t.hi, t.loR, t.hiR ) );
-    double[ ][ ][ ] out = new double[ P ][ Q ][ R ];
-    for( int i = 0; i < P; i++ )
-      for( int j = 0; j < Q; j++ )
-        System.arraycopy( y, ( i * Q + j ) * R, out[ i ][ j ], 0, R );
-    return out;
+    return HipNative.run3d( _kind, _taps, false, false, s, lvlP, lvlQ, lvlR );
   }
 }

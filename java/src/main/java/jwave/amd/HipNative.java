@@ -111,6 +111,12 @@ public final class HipNative {
       int p, int q, int r, int lvlP, int lvlQ, int lvlR, int L, int tw, double scale,
       double[ ] lo, double[ ] hi, double[ ] loR, double[ ] hiR );
 
+  /** ParallelTransform's 3-D reverse order: the P axis first, then the slices
+   *  (ParallelTransform.java:183-216). */
+  static native int transform3dPt( long ctx, int kind, double[ ] x, double[ ] y, int p, int q,
+      int r, int lvlP, int lvlQ, int lvlR, int L, int tw, double scale, double[ ] lo,
+      double[ ] hi, double[ ] loR, double[ ] hiR );
+
   /** wv = (J+1)*n doubles, rows W_1..W_J, V_J. */
   static native int modwt( long ctx, boolean forward, double[ ] x, double[ ] wv, int n, int J,
       int L, int tw, double[ ] lo, double[ ] hi, double[ ] loR, double[ ] hiR );
@@ -142,6 +148,44 @@ public final class HipNative {
     double[ ] out = new double[ rows * cols ];
     for( int i = 0; i < rows; i++ )
       System.arraycopy( m[ i ], 0, out, i * cols, cols );
+    return out;
+  }
+
+  static boolean fits3d( double[ ][ ][ ] s ) {
+    long P = s.length, Q = P == 0 ? 0 : s[ 0 ].length, R = Q == 0 ? 0 : s[ 0 ][ 0 ].length;
+    return fitsArray( P * Q, R );
+  }
+
+  /** BasicTransform.forward|reverse(double[][], lvlM, lvlN) in one call. */
+  static double[ ][ ] run2d( int kind, Taps t, boolean fwd, double[ ][ ] m, int lvlM, int lvlN )
+      throws JWaveException {
+    int rows = m.length, cols = rows == 0 ? 0 : m[ 0 ].length;
+    double[ ] x = pack( m ), y = new double[ x.length ];
+    check( transform2d( ctx( ), kind, fwd, x, y, rows, cols, lvlM, lvlN, t.L, t.tw, t.scale,
+        t.lo, t.hi, t.loR, t.hiR ) );
+    return unpack( y, rows, cols );
+  }
+
+  /** BasicTransform.forward|reverse(double[][][], lvlP, lvlQ, lvlR) in one
+   *  call; pt: ParallelTransform's reverse order (P axis first). */
+  static double[ ][ ][ ] run3d( int kind, Taps t, boolean fwd, boolean pt, double[ ][ ][ ] s,
+      int lp, int lq, int lr ) throws JWaveException {
+    int P = s.length, Q = P == 0 ? 0 : s[ 0 ].length, R = Q == 0 ? 0 : s[ 0 ][ 0 ].length;
+    double[ ] x = new double[ P * Q * R ];
+    for( int i = 0; i < P; i++ )
+      for( int j = 0; j < Q; j++ )
+        System.arraycopy( s[ i ][ j ], 0, x, ( i * Q + j ) * R, R );
+    double[ ] y = new double[ x.length ];
+    if( pt )
+      check( transform3dPt( ctx( ), kind, x, y, P, Q, R, lp, lq, lr, t.L, t.tw, t.scale, t.lo,
+          t.hi, t.loR, t.hiR ) );
+    else
+      check( transform3d( ctx( ), kind, fwd, x, y, P, Q, R, lp, lq, lr, t.L, t.tw, t.scale,
+          t.lo, t.hi, t.loR, t.hiR ) );
+    double[ ][ ][ ] out = new double[ P ][ Q ][ R ];
+    for( int i = 0; i < P; i++ )
+      for( int j = 0; j < Q; j++ )
+        System.arraycopy( y, ( i * Q + j ) * R, out[ i ][ j ], 0, R );
     return out;
   }
 

@@ -8,7 +8,7 @@ import jwave.exceptions.JWaveException;
 import jwave.transforms.WaveletPacketTransform;
 import jwave.transforms.wavelets.Wavelet;
 
-public class HipWaveletPacketTransform extends WaveletPacketTransform {
+public class HipWaveletPacketTransform extends WaveletPacketTransform implements HipTransform {
 
   private final HipNative.Taps _taps;
 
@@ -49,7 +49,38 @@ public class HipWaveletPacketTransform extends WaveletPacketTransform {
     return HipNative.unpack( mat, rows, n );
   }
 
-  HipNative.Taps taps( ) { return _taps; }
+  @Override public HipNative.Taps taps( ) { return _taps; }
+
+  @Override public int kind( ) { return 1; }
+
+  // 2-D / 3-D (BasicTransform.java:361-474, 509-659) in one native call each
+  @Override public double[ ][ ] forward( double[ ][ ] m, int lvlM, int lvlN )
+      throws JWaveException {
+    if( _taps == null || !HipNative.fitsArray( m.length, m.length == 0 ? 0 : m[ 0 ].length ) )
+      return super.forward( m, lvlM, lvlN );
+    return HipNative.run2d( 1, _taps, true, m, lvlM, lvlN );
+  }
+
+  @Override public double[ ][ ] reverse( double[ ][ ] m, int lvlM, int lvlN )
+      throws JWaveException {
+    if( _taps == null || !HipNative.fitsArray( m.length, m.length == 0 ? 0 : m[ 0 ].length ) )
+      return super.reverse( m, lvlM, lvlN );
+    return HipNative.run2d( 1, _taps, false, m, lvlM, lvlN );
+  }
+
+  @Override public double[ ][ ][ ] forward( double[ ][ ][ ] s, int lvlP, int lvlQ, int lvlR )
+      throws JWaveException {
+    if( _taps == null || !HipNative.fits3d( s ) )
+      return super.forward( s, lvlP, lvlQ, lvlR );
+    return HipNative.run3d( 1, _taps, true, false, s, lvlP, lvlQ, lvlR );
+  }
+
+  @Override public double[ ][ ][ ] reverse( double[ ][ ][ ] s, int lvlP, int lvlQ, int lvlR )
+      throws JWaveException {
+    if( _taps == null || !HipNative.fits3d( s ) )
+      return super.reverse( s, lvlP, lvlQ, lvlR );
+    return HipNative.run3d( 1, _taps, false, false, s, lvlP, lvlQ, lvlR );
+  }
 
   /** Every row (one signal each, equal lengths) with the same level: one
    *  native call instead of one per signal. */

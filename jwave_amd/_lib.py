@@ -90,7 +90,10 @@ for _n in ("wpt2d_fwd", "wpt2d_rev"):
 for _n in ("fwt3d_fwd", "fwt3d_rev"):
     for _s in ("", "_dev"):
         _SIGS["jwv_%s_f64%s" % (_n, _s)] = [_dp, _dp, _i64, _i64, _i64, _int, _int, _int, _TP, _CTX]
-for _n in ("wpt3d_fwd", "wpt3d_rev"):
+for _s in ("", "_dev"):
+    _SIGS["jwv_fwt3d_rev_pt_f64%s" % _s] = [_dp, _dp, _i64, _i64, _i64, _int, _int, _int, _TP,
+                                            _CTX]
+for _n in ("wpt3d_fwd", "wpt3d_rev", "wpt3d_rev_pt"):
     _SIGS["jwv_%s_f64" % _n] = [_dp, _dp, _i64, _i64, _i64, _int, _int, _int, _TP, _CTX]
 for _n in ("fwt_axis_fwd", "fwt_axis_rev", "wpt_axis_fwd", "wpt_axis_rev"):
     _SIGS["jwv_%s_f64_dev" % _n] = [_dp, _dp, _i64, _i64, _i64, _int, _TP, _CTX]

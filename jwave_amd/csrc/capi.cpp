@@ -942,9 +942,11 @@ void body_2d(jwv_ctx* c, Kind k, bool fwd, const Bank& b, const double* x, doubl
 }
 
 // BasicTransform.java:509-560 / 602-659: slice 2-D transform with (lvlP on the
-// Q axis, lvlQ on the R axis), then the P axis with lvlR.
+// Q axis, lvlQ on the R axis), then the P axis with lvlR.  pt: the reverse in
+// ParallelTransform's order (ParallelTransform.java:183-216): the P axis
+// first, then the slices.
 void body_3d(jwv_ctx* c, Kind k, bool fwd, const Bank& b, const double* x, double* y, int64_t P,
-             int64_t Q, int64_t R, int lvl_p, int lvl_q, int lvl_r) {
+             int64_t Q, int64_t R, int lvl_p, int lvl_q, int lvl_r, bool pt = false) {
   if (P == 0 || Q == 0 || R == 0) return;
   double* tmp = grow(c, c->big, (size_t)(P * Q * R));
   const AxisView vr = cview(R, 1), vq = cview(Q, R), vp = cview(P, Q * R);
@@ -953,10 +955,14 @@ void body_3d(jwv_ctx* c, Kind k, bool fwd, const Bank& b, const double* x, doubl
     f(c, b, Axis{x, vr, y, vr, P * Q, (int)R, 1}, lvl_q);          // rows of each slice
     f(c, b, Axis{y, vq, tmp, vq, P, (int)Q, (int)R}, lvl_p);       // columns of each slice
     f(c, b, Axis{tmp, vp, y, vp, 1, (int)P, (int)(Q * R)}, lvl_r); // along i
-  } else {
+  } else if (!pt) {
     f(c, b, Axis{x, vq, y, vq, P, (int)Q, (int)R}, lvl_p);         // slice columns
     f(c, b, Axis{y, vr, tmp, vr, P * Q, (int)R, 1}, lvl_q);        // slice rows
     f(c, b, Axis{tmp, vp, y, vp, 1, (int)P, (int)(Q * R)}, lvl_r); // along i
+  } else {
+    f(c, b, Axis{x, vp, y, vp, 1, (int)P, (int)(Q * R)}, lvl_r);   // along i
+    f(c, b, Axis{y, vq, tmp, vq, P, (int)Q, (int)R}, lvl_p);       // slice columns
+    f(c, b, Axis{tmp, vr, y, vr, P * Q, (int)R, 1}, lvl_q);        // slice rows
   }
 }
 
@@ -1642,10 +1648,15 @@ JWV_2D(jwv_wpt2d_rev_f64, Kind::WPT, false)
 JWV_2D_DEV(jwv_wpt2d_fwd_f64_dev, Kind::WPT, true)
 JWV_2D_DEV(jwv_wpt2d_rev_f64_dev, Kind::WPT, false)
 
-static void check_3d(Kind k, bool fwd, int64_t P, int64_t Q, int64_t R, int lp, int lq, int lr) {
+static void check_3d(Kind k, bool fwd, int64_t P, int64_t Q, int64_t R, int lp, int lq, int lr,
+                     bool pt = false) {
   if (P < 0 || Q < 0 || R < 0) throw Fail{JWV_ERR_BAD_CALL, "negative dimension"};
   if (P == 0 || Q == 0 || R == 0) return;
-  if (fwd) {
+  if (pt) {  // ParallelTransform reverse: P axis, then slice columns, slice rows
+    check_1d(k, false, P, lr);
+    check_1d(k, false, Q, lp);
+    check_1d(k, false, R, lq);
+  } else if (fwd) {
     check_1d(k, true, R, lq);
     check_1d(k, true, Q, lp);
     check_1d(k, true, P, lr);
@@ -1657,22 +1668,23 @@ static void check_3d(Kind k, bool fwd, int64_t P, int64_t Q, int64_t R, int lp, 
   if (P * Q * R > (int64_t(1) << 33)) throw Fail{JWV_ERR_BAD_CALL, "volume too large"};
 }
 
-#define JWV_3D(NAME, KIND, FWD, DEV)                                                                    \
+#define JWV_3D(NAME, KIND, FWD, DEV) JWV_3DX(NAME, KIND, FWD, DEV, false)
+#define JWV_3DX(NAME, KIND, FWD, DEV, PT)                                                         \
   int NAME(const double* x, double* y, int64_t P, int64_t Q, int64_t R, int lp, int lq, int lr,   \
            const jwv_taps* t, jwv_ctx* c) {                                                       \
     return guarded(c, [&] {                                                                       \
       const Bank b = make_bank(t);                                                                \
-      check_3d(KIND, FWD, P, Q, R, lp, lq, lr);                                                         \
+      check_3d(KIND, FWD, P, Q, R, lp, lq, lr, PT);                                               \
       if (P == 0 || Q == 0 || R == 0) return;                                                     \
       check_ptrs(x, y);                                                                           \
       const size_t tot = (size_t)(P * Q * R);                                                     \
       if (DEV) {                                                                                  \
         need_device_ptrs(c, x, y);                                                                \
         check_overlap(x, tot, y, tot);                                                            \
-        body_3d(c, KIND, FWD, b, x, y, P, Q, R, lp, lq, lr);                                      \
+        body_3d(c, KIND, FWD, b, x, y, P, Q, R, lp, lq, lr, PT);                                  \
       } else {                                                                                    \
         staged(c, x, tot, y, tot, [&](const double* dx, double* dy) {                             \
-          body_3d(c, KIND, FWD, b, dx, dy, P, Q, R, lp, lq, lr);                                  \
+          body_3d(c, KIND, FWD, b, dx, dy, P, Q, R, lp, lq, lr, PT);                              \
         });                                                                                       \
       }                                                                                           \
     });                                                                                           \
@@ -1683,6 +1695,9 @@ JWV_3D(jwv_fwt3d_fwd_f64_dev, Kind::FWT, true, true)
 JWV_3D(jwv_fwt3d_rev_f64_dev, Kind::FWT, false, true)
 JWV_3D(jwv_wpt3d_fwd_f64, Kind::WPT, true, false)
 JWV_3D(jwv_wpt3d_rev_f64, Kind::WPT, false, false)
+JWV_3DX(jwv_fwt3d_rev_pt_f64, Kind::FWT, false, false, true)
+JWV_3DX(jwv_fwt3d_rev_pt_f64_dev, Kind::FWT, false, true, true)
+JWV_3DX(jwv_wpt3d_rev_pt_f64, Kind::WPT, false, false, true)
 
 // ---- CompressorMagnitude / denoise ---------------------------------------------------
 namespace {

@@ -254,9 +254,12 @@ def transform_2d(x, wavelet, lvl_m, lvl_n, forward=True, ctx=None, kind="fwt"):
                 (r, c), (r, c, int(lvl_m), int(lvl_n), _TapsHolder.of(wavelet)))
 
 
-def transform_3d(x, wavelet, lvl_p, lvl_q, lvl_r, forward=True, ctx=None, kind="fwt"):
+def transform_3d(x, wavelet, lvl_p, lvl_q, lvl_r, forward=True, ctx=None, kind="fwt",
+                 pt_order=False):
+    """3-D transform (BasicTransform.java:509-659).  pt_order: the reverse in
+    ParallelTransform's order, P axis first (jwv_*3d_rev_pt_f64)."""
     p, q, r = x.shape
-    d = "fwd" if forward else "rev"
+    d = "fwd" if forward else ("rev_pt" if pt_order else "rev")
     dev_name = "jwv_%s3d_%s_f64_dev" % (kind, d) if kind == "fwt" else None
     if _is_torch(x) and getattr(x, "is_cuda", False) and dev_name is None:
         raise JWaveError("device 3-D packet transform is not exported")
@@ -815,6 +818,82 @@ class AncientEgyptianDecomposition(BasicTransform):
 
     def reverse_1d(self, arr, level=None):
         return self._run(arr, False)
+
+
+class ParallelTransform(BasicTransform):
+    """jwave.transforms.ParallelTransform (ParallelTransform.java:23-403) over
+    a GPU transform.  The reference forks row / column / line tasks that call
+    the wrapped transform once per line (RowTransformTask :247-263,
+    ColumnTransformTask :307-330, Space3DTransformTask :380-397): wrapped
+    around a GPU transform that would be one native call per line.  Here every
+    2-D / 3-D call is ONE native call with the reference's result:
+
+    * 1-D, 2-D and the 3-D forward: the wrapped transform's own methods
+      (rows with lvlN then columns with lvlM; slices then the P axis) -- the
+      same order the ForkJoin tasks use, so the same doubles;
+    * 3-D reverse: the P axis FIRST, then each slice's 2-D reverse
+      (ParallelTransform.java:183-216), which BasicTransform does the other
+      way round (slices first): jwv_*3d_rev_pt_f64.
+
+    Errors carry the reference's prefixes ("Error in parallel 2D forward
+    transform: ..."), for matrices the reference runs in parallel (both
+    dimensions >= MIN_PARALLEL_SIZE = 16; smaller 2-D inputs go straight to
+    the wrapped transform, as :73-76 do)."""
+
+    MIN_PARALLEL_SIZE = 16
+
+    def __init__(self, transform, parallelism=None):
+        super().__init__(transform._wavelet, transform._ctx)
+        self._transform = transform
+        self._parallelism = parallelism
+        self.kind = transform.kind
+        self._name = transform.getName()
+
+    def _check_1d(self, n, level, fwd):
+        return self._transform._check_1d(n, level, fwd)
+
+    def forward_1d(self, arr, *levels):
+        return self._transform.forward_1d(arr, *levels)
+
+    def reverse_1d(self, arr, *levels):
+        return self._transform.reverse_1d(arr, *levels)
+
+    def _par(self, what, fn, *args):
+        try:
+            return fn(*args)
+        except JWaveException as e:
+            raise JWaveException("Error in parallel %s transform: %s" % (what, e.getMessage()))
+
+    def forward_2d(self, m, lvl_m=None, lvl_n=None):
+        r, c = m.shape
+        if r < self.MIN_PARALLEL_SIZE or c < self.MIN_PARALLEL_SIZE:
+            return self._transform.forward_2d(m, lvl_m, lvl_n)
+        return self._par("2D forward", self._transform.forward_2d, m, lvl_m, lvl_n)
+
+    def reverse_2d(self, m, lvl_m=None, lvl_n=None):
+        r, c = m.shape
+        if r < self.MIN_PARALLEL_SIZE or c < self.MIN_PARALLEL_SIZE:
+            return self._transform.reverse_2d(m, lvl_m, lvl_n)
+        return self._par("2D reverse", self._transform.reverse_2d, m, lvl_m, lvl_n)
+
+    def forward_3d(self, s, lvl_p=None, lvl_q=None, lvl_r=None):
+        return self._par("3D forward", self._transform.forward_3d, s, lvl_p, lvl_q, lvl_r)
+
+    def reverse_3d(self, s, lvl_p=None, lvl_q=None, lvl_r=None):
+        def run():
+            p, q, r = s.shape
+            lp, lq, lr = lvl_p, lvl_q, lvl_r
+            if lp is None:
+                lp, lq, lr = get_exponent(p), get_exponent(q), get_exponent(r)
+            self._check_1d(p, lr, False)  # the P-axis task runs first (:191)
+            self._check_1d(q, lp, False)
+            self._check_1d(r, lq, False)
+            return transform_3d(s, self._wavelet, lp, lq, lr, False, self._ctx, self.kind,
+                                pt_order=True)
+        return self._par("3D reverse", run)
+
+    def shutdown(self):
+        """ParallelTransform.shutdown (:399-401): no pool to stop here."""
 
 
 class Transform:

@@ -123,6 +123,8 @@ T3(jwv_fwt3d_fwd_f64, 13)
 T3(jwv_fwt3d_rev_f64, 14)
 T3(jwv_wpt3d_fwd_f64, 15)
 T3(jwv_wpt3d_rev_f64, 16)
+T3(jwv_fwt3d_rev_pt_f64, 22)
+T3(jwv_wpt3d_rev_pt_f64, 23)
 
 int jwv_modwt_fwd_f64(const double* x, double* wv, int64_t n, int J, const jwv_taps* t,
                       jwv_ctx* c) {

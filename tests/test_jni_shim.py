@@ -73,10 +73,13 @@ def _declare(lib):
     lib.Java_jwave_amd_HipNative_transform2d.argtypes = [P, P, J, I, B, P, P, I, I, I, I] + taps
     lib.Java_jwave_amd_HipNative_transform3d.argtypes = ([P, P, J, I, B, P, P, I, I, I, I, I, I]
                                                          + taps)
+    lib.Java_jwave_amd_HipNative_transform3dPt.argtypes = ([P, P, J, I, P, P, I, I, I, I, I, I]
+                                                           + taps)
     lib.Java_jwave_amd_HipNative_modwt.argtypes = [P, P, J, B, P, P, I, I, I, I, P, P, P, P]
     lib.Java_jwave_amd_HipNative_aed.argtypes = [P, P, J, I, B, P, P] + taps
     lib.Java_jwave_amd_HipNative_decompose.argtypes = [P, P, J, I, P, P] + taps
-    for f in ("transform1d", "transformBatch", "transform2d", "transform3d", "modwt", "aed",
+    for f in ("transform1d", "transformBatch", "transform2d", "transform3d", "transform3dPt",
+              "modwt", "aed",
               "decompose", "ctxCreate"):
         getattr(lib, "Java_jwave_amd_HipNative_" + f).restype = I
     return lib
@@ -198,6 +201,12 @@ def test_batch_2d_3d_aed_decompose_marshaling(jvm):
     assert jvm.native("transform3d", ctx, 1, 1, jx, jy, 4, 8, 8, 1, 2, 3, *jvm.taps(w)) == 0
     c = jvm.last()
     assert c.name == b"jwv_wpt3d_fwd_f64" and list(c.a) == [4, 8, 8, 1, 2, 3]
+    for kind, name, k in [(0, b"jwv_fwt3d_rev_pt_f64", 22), (1, b"jwv_wpt3d_rev_pt_f64", 23)]:
+        jy = jvm.empty(256)
+        assert jvm.native("transform3dPt", ctx, kind, jx, jy, 4, 8, 8, 1, 2, 3, *jvm.taps(w)) == 0
+        c = jvm.last()
+        assert c.name == name and list(c.a) == [4, 8, 8, 1, 2, 3]
+        assert np.array_equal(jvm.read(jy, 256), 2 * x + k)
     jx7, jy7 = jvm.darray(x[:7]), jvm.empty(7)
     assert jvm.native("aed", ctx, 1, 0, jx7, jy7, *jvm.taps(w)) == 0
     c = jvm.last()

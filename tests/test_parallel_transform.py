@@ -1,0 +1,115 @@
+"""ParallelTransform over a GPU transform (ParallelTransform.java:23-403).
+
+The reference's ForkJoin tasks call the wrapped transform once per row,
+column or line (RowTransformTask :247-263, ColumnTransformTask :307-330,
+Space3DTransformTask :380-397).  jwave_amd.ParallelTransform (and the Java
+HipParallelTransform) make each 2-D / 3-D call ONE native call with the
+reference's result; its 3-D reverse keeps the reference's order (the P axis
+first, then the slices), which BasicTransform.reverse does the other way
+round.
+"""
+import numpy as np
+import pytest
+
+import jwave_amd as jw
+from jwave_amd import transforms as T
+from jwave_amd.exceptions import JWaveException
+
+
+@pytest.fixture
+def spy(monkeypatch):
+    calls = []
+
+    def fake_run(fn_host, fn_dev, ctx, x, out_shape, args):
+        calls.append(fn_host)
+        return np.zeros(out_shape)
+
+    monkeypatch.setattr(T, "_run", fake_run)
+    return calls
+
+
+def _pt(kind="fwt", name="Daubechies4"):
+    w = jw.by_class(name)
+    inner = jw.FastWaveletTransform(w) if kind == "fwt" else jw.WaveletPacketTransform(w)
+    return jw.ParallelTransform(inner)
+
+
+@pytest.mark.parametrize("kind", ["fwt", "wpt"])
+def test_one_native_call_per_matrix(spy, kind):
+    pt = _pt(kind)
+    m = np.ones((256, 512))
+    pt.forward(m)
+    pt.reverse(m)
+    pt.forward(m, 3, 4)
+    s = np.ones((32, 32, 32))  # default levels map lvlP onto the Q axis (:487-493)
+    pt.forward(s)
+    pt.reverse(s)
+    pt.forward(np.ones((8, 512)))  # below MIN_PARALLEL_SIZE: the wrapped transform
+    assert spy == ["jwv_%s2d_fwd_f64" % kind, "jwv_%s2d_rev_f64" % kind, "jwv_%s2d_fwd_f64" % kind,
+                   "jwv_%s3d_fwd_f64" % kind, "jwv_%s3d_rev_pt_f64" % kind,
+                   "jwv_%s2d_fwd_f64" % kind]
+    # the reference would call the wrapped 1-D transform 256 + 512 times for
+    # the first matrix alone (one task call per row and per column)
+
+
+def test_1d_delegates(spy):
+    pt = _pt()
+    pt.forward(np.ones(1024))
+    pt.reverse(np.ones(1024), 3)
+    assert spy == ["jwv_fwt_fwd_f64", "jwv_fwt_rev_f64"]
+
+
+def test_error_prefixes(spy):
+    pt = _pt()
+    with pytest.raises(JWaveException, match="^Error in parallel 2D forward transform: "
+                       "FastWaveletTransform#forward - given level is out of range"):
+        pt.forward(np.ones((64, 64)), 7, 2)
+    with pytest.raises(JWaveException, match="^Error in parallel 3D reverse transform: "):
+        pt.reverse(np.ones((16, 16, 16)), 1, 1, 9)
+    # below MIN_PARALLEL_SIZE the wrapped transform's own exception, unwrapped
+    with pytest.raises(jw.JWaveFailure, match="^FastWaveletTransform#forward"):
+        pt.forward(np.ones((8, 8)), 4, 1)
+    assert spy == []
+
+
+def test_pt_reverse_checks_p_axis_first(spy):
+    """The P-axis task runs first (ParallelTransform.java:191), so its level
+    error is the one reported when several dimensions are bad."""
+    pt = _pt()
+    with pytest.raises(JWaveException, match="3D reverse.*out of range"):
+        pt.reverse(np.ones((16, 16, 16)), 9, 9, 9)
+
+
+# ------------------------------------------------------------------ GPU parity
+def _axis(kind, fwd, w, a, axis, level):
+    import oracle
+    m = np.moveaxis(a, axis, -1)
+    shp = m.shape
+    out = oracle.batch(kind, fwd, w, np.ascontiguousarray(m.reshape(-1, shp[-1])), level)
+    return np.moveaxis(out.reshape(shp), -1, axis)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["fwt", "wpt"])
+@pytest.mark.parametrize("name", ["Haar1", "Daubechies4", "Symlet8"])
+def test_parallel_transform_gpu_parity(kind, name):
+    import oracle
+    w = jw.by_class(name)
+    pt = _pt(kind, name)
+    rng = np.random.default_rng(7)
+    m = rng.standard_normal((64, 128))
+    got = pt.forward(m)
+    ref = oracle.transform_2d_par(kind, True, w, m, 6, 7, 4)
+    assert np.array_equal(got, ref)
+    assert np.array_equal(pt.reverse(ref), oracle.transform_2d_par(kind, False, w, ref, 6, 7, 4))
+    s = rng.standard_normal((16, 32, 64))
+    lp, lq, lr = 3, 5, 2
+    f = pt.forward(s, lp, lq, lr)
+    assert np.array_equal(f, oracle.transform_3d(kind, True, w, s, lp, lq, lr))
+    # reverse: P axis (lvlR) first, then slice columns (lvlP), slice rows (lvlQ)
+    ref = _axis(kind, False, w, f, 0, lr)
+    ref = _axis(kind, False, w, ref, 1, lp)
+    ref = _axis(kind, False, w, ref, 2, lq)
+    got = pt.reverse(f, lp, lq, lr)
+    assert np.array_equal(got, ref)
+    assert np.abs(got - s).max() < 1e-12
