@@ -28,8 +28,8 @@
 
 #include "../../include/jwave_hip.h"
 #include "jwv_launch.hpp"
-#include "jwv_stream.hpp"
 #include "jwv_modwt1.hpp"
+#include "jwv_tail.hpp"
 
 using jwv::AxisView;
 using jwv::Bank;
@@ -404,23 +404,13 @@ bool try_rev_chain(jwv_ctx* c, const Bank& b, const Axis& a, int h0) {
 // Resident-pass cap of an FWT axis transform.  Many contiguous signals (2-D
 // rows, batches) can instead run their top levels through the C = 1 tile
 // kernels and only a short tail resident (config 3 rows: 2.21 -> 1.99 ms per
-// step at 2048).  env JWV_ROWCAP (elements; >= kResCap1 = always resident).
+// step at 2048).
 // Resident reverse cap of row batches on the fwt1 path: the tile pass above
-// it takes the remaining levels (env JWV_REVROWTAIL: 256 | 512 | 1024).
-int rev_row_tail() {
-  static const int t = [] {
-    const char* v = std::getenv("JWV_REVROWTAIL");
-    const int x = v ? std::atoi(v) : Geo::kFwt1RevTail;
-    return (x == 256 || x == 512 || x == 1024) ? x : Geo::kFwt1RevTail;
-  }();
-  return t;
-}
+// it takes the remaining levels (1024; 256 and 512 measured slower).
+int rev_row_tail() { return Geo::kFwt1RevTail; }
 
 int fwt_res_cap(int C, int64_t outer) {
-  static const int rowcap = [] {
-    const char* v = std::getenv("JWV_ROWCAP");
-    return v ? std::atoi(v) : 2048;
-  }();
+  constexpr int rowcap = 2048;
   if (C == 1 && outer >= 64 && rowcap >= 64 && rowcap < Geo::kResCap1) return rowcap;
   return Geo::res_cap(C);
 }
@@ -434,29 +424,7 @@ int fwt_res_cap(int C, int64_t outer) {
 // Infinity Cache (config 2 steady state over 3 alternating runs: 111.3-113.5
 // -> 109.0-111.3 us/step); forward outputs stay cacheable (nt on them: the
 // reverse that reads them next took 123 us/step).
-int store_pol_dir(int rev, bool final = false) {
-  static const int p[2] = {[] {
-                             const char* e = std::getenv("JWV_STPOL_F");
-                             return e ? std::atoi(e) : Geo::store_pol();
-                           }(),
-                           [] {
-                             const char* e = std::getenv("JWV_STPOL_R");
-                             return e ? std::atoi(e) : -1;
-                           }()};
-  int v = p[rev & 1];
-  if (rev && v < 0) v = final ? 2 : Geo::store_pol();
-  return v < 0 || v > 2 ? 0 : v;
-}
-
-// env JWV_FWD1S (default 0): the first forward pass of contiguous signals on
-// the persistent grid of fwt1_stream.hpp instead of one block per tile
-bool fwd_stream1() {
-  static const bool v = [] {
-    const char* e = std::getenv("JWV_FWD1S");
-    return e && std::atoi(e) != 0;
-  }();
-  return v;
-}
+int store_pol_dir(int rev, bool final = false) { return rev && final ? 2 : 0; }
 
 void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
   const int nlev = fwd_levels(a.len, b.tw, level);
@@ -510,20 +478,12 @@ void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
     const AxisView av = last ? a.dv : cview(h >> K, a.inner);
     jwv::TileArgs t{cur, cv, nullptr, {}, a.dst, a.dv, ad, av, h, K, a.outer, a.inner,
                     dma_view(cur, cv, C, a.inner),
-                    (h == a.len ? store_pol_dir(0) | (a.outer == 1 ? Geo::tile_desc(0) : 0) : 0) |
-                        Geo::tile_walk(),
+                    Geo::tile_walk(),
                     first1 && h == a.len && Geo::fwd1_first_t() != Geo::kFwt1T
                         ? Geo::fwd1_first_t() : 0};
     { ProfScope ps_(c, h == a.len ? K_FWT_FWD_TILE : K_FWT_FWD_TILE_DEEP,
                     16.0 * a.outer * h * a.inner);
-      hipError_t e = hipSuccess;
-      // the full-length pass as a persistent double-buffered grid
-      // (fwt1_stream.hpp) where it covers the case
-      const bool st = C == 1 && h == a.len && fwd_stream1() &&
-                      (use_fma(c) ? jwv::fused::fwt_fwd_stream1(b, t, c->stream, e)
-                                  : jwv::exact::fwt_fwd_stream1(b, t, c->stream, e));
-      if (!st) e = jwv::launch_fwt_fwd_tile(b, use_fma(c), C, t, c->stream);
-      hipchk(e, "fwt_fwd_tile"); }
+      hipchk(jwv::launch_fwt_fwd_tile(b, use_fma(c), C, t, c->stream), "fwt_fwd_tile"); }
     cur = ad;
     cv = av;
     h >>= K;
@@ -615,9 +575,7 @@ void fwt_rev_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
     const AxisView ov = last ? a.dv : cview(hK, a.inner);
     jwv::TileArgs t{acur, acv, a.src, a.sv, out, ov, nullptr, {}, h1, K, a.outer, a.inner,
                     dma_view(acur, acv, C, a.inner) && dma_view(a.src, a.sv, C, a.inner),
-                    (last ? store_pol_dir(1, a.outer == 1 && a.inner == 1) |
-                                (a.outer == 1 ? Geo::tile_desc(1) : 0)
-                          : 0) |
+                    (last ? store_pol_dir(1, a.outer == 1 && a.inner == 1) : 0) |
                         Geo::tile_walk()};
     { ProfScope ps_(c, last ? K_FWT_REV_TILE : K_FWT_REV_TILE_DEEP, 16.0 * a.outer * hK * a.inner);
     hipchk(jwv::launch_fwt_rev_tile(b, use_fma(c), C, t, c->stream), "fwt_rev_tile"); }
@@ -1081,15 +1039,9 @@ void check_modwt(int64_t n, int J) {
   }
 }
 
-// env JWV_MODWT_CT (default 1): the compile-time-geometry MODWT tiles
-// (modwt1_kernels.hpp) where they cover the case; 0 = the runtime tiles.
-bool modwt_ct() {
-  static const bool v = [] {
-    const char* e = std::getenv("JWV_MODWT_CT");
-    return e ? std::atoi(e) != 0 : true;
-  }();
-  return v;
-}
+// The compile-time-geometry MODWT tiles (modwt1_kernels.hpp, modwt_pipe.hpp)
+// where they cover the case, else the runtime tiles.
+bool modwt_ct() { return true; }
 
 int64_t modwt_halo(int L, int j0, int j1) {
   return (int64_t)(L - 1) * ((int64_t(1) << j1) - (int64_t(1) << (j0 - 1)));
@@ -1184,94 +1136,28 @@ void need_device_ptrs(jwv_ctx* c, const double* x, const double* y) {
 
 // dispatch shims for the two math modes
 namespace jwv {
-static int env_int(const char* name, int dflt) {
-  const char* v = std::getenv(name);
-  return v ? std::atoi(v) : dflt;
-}
-int Geo::fwd_t1() {
-  static const int t = env_int("JWV_FWD_T", kFwtT1) == 2048 ? 2048 : kFwtT1;
-  return t;
-}
-int Geo::rev_t1() {
-  static const int t = env_int("JWV_REV_T", kFwtT1) == 2048 ? 2048 : kFwtT1;
-  return t;
-}
-bool Geo::fwd_stream() {
-  static const bool p = env_int("JWV_FWD_STREAM", 0) != 0;
-  return p;
-}
-int Geo::stream_blocks_per_cu() {
-  static const int n = env_int("JWV_STREAM_BPC", 2);
-  return n < 1 ? 1 : (n > 8 ? 8 : n);
-}
-bool Geo::fwt1() {
-  static const bool p = env_int("JWV_FWT1", 1) != 0;
-  return p;
-}
-int Geo::slab_order() {
-  static const int o = env_int("JWV_SLAB_ORDER", 1) ? 1 : 0;
-  return o;
-}
-int Geo::store_pol() {
-  static const int p = env_int("JWV_STPOL", 0);
-  return p < 0 || p > 2 ? 0 : p;
-}
-// sp bit 2 for the big pass of one long signal: env JWV_TILE_DESC bit 0 =
-// forward, bit 1 = reverse walks its XCD chunks last-to-first.
-int Geo::tile_desc(int rev) {
-  static const int d = env_int("JWV_TILE_DESC", 0);
-  return ((d >> rev) & 1) << 2;
-}
-// Default G = 64 (config 2, one MI355X, alternating runs on one box: forward
-// big pass 53.7 -> 46.0 us by rocprofv3, 0.1231-0.1256 -> 0.1146-0.1182
-// ms/step; G = 32 / 128 within noise of 64; JWV_TILE_G=0 restores the
-// chunked walk).
-int Geo::tile_walk() {
-  static const int w = [] {
-    const int g = env_int("JWV_TILE_G", 64);
-    if (g <= 0 || (g & (g - 1)) || g > (1 << 20)) return 0;
-    int gs = 0;
-    while ((1 << gs) < g) ++gs;
-    return 8 | (gs << 8);
-  }();
-  return w;
-}
-int Geo::fwd1_first_t() {
-  static const int t = env_int("JWV_FWD1T", kFwt1T) == 1024 ? 1024 : kFwt1T;
-  return t;
-}
-int Geo::fwd1_first_k() {
-  static const int k = [] {
-    const int v = env_int("JWV_FWD1K", kFwtK1);
-    return fwd1_first_t() == 1024 ? std::max(4, std::min(6, v)) : std::max(1, std::min(kFwt1KMax, v));
-  }();
-  return k;
-}
-int Geo::fwd1_tail() {
-  static const int t = [] {
-    const int v = env_int("JWV_FWD1TAIL", kFwt1FwdTail);
-    return (v == 256 || v == 512 || v == 1024 || v == 2048) ? v : kFwt1FwdTail;
-  }();
-  return t;
-}
-bool Geo::fwt8() {
-  static const bool p = env_int("JWV_FWT8", 1) != 0;
-  return p;
-}
-int Geo::stream_ntc() {
-  static const int n = env_int("JWV_STREAM_NTC", 512) == 256 ? 256 : 512;
-  return n;
-}
-bool Geo::rev_pref() {
-  static const bool p = env_int("JWV_REV_PREF", 0) != 0;
-  return p;
-}
+// Plan geometry: the measured defaults.  The alternatives
+// these once selected through environment variables were measured slower
+// and removed (git history keeps them).
+int Geo::fwd_t1() { return kFwtT1; }
+int Geo::rev_t1() { return kFwtT1; }
+bool Geo::fwt1() { return true; }
+// slab-fastest walk of the C = 8 tiles (config 3: 1.76 -> 1.58 ms/step)
+int Geo::slab_order() { return 1; }
+int Geo::store_pol() { return 0; }
+int Geo::tile_desc(int) { return 0; }
+// Grouped one-front walk, G = 64 (config 2, one MI355X, alternating runs on
+// one box: forward big pass 53.7 -> 46.0 us by rocprofv3, 0.1231-0.1256 ->
+// 0.1146-0.1182 ms/step; G = 32 / 128 within noise of 64).
+int Geo::tile_walk() { return 8 | (6 << 8); }
+int Geo::fwd1_first_t() { return kFwt1T; }
+int Geo::fwd1_first_k() { return std::max(1, std::min(kFwt1KMax, kFwtK1)); }
+int Geo::fwd1_tail() { return kFwt1FwdTail; }
+bool Geo::fwt8() { return true; }
+bool Geo::rev_pref() { return false; }
 #define JWV_MODE2(name, ...) \
   return fma ? fused::name(__VA_ARGS__) : exact::name(__VA_ARGS__)
-int ChainGeo::default_plan() {
-  static const int p = env_int("JWV_PLAN", JWV_PLAN_REV_HEAD | JWV_PLAN_FWD_TAIL) & 15;
-  return p;
-}
+int ChainGeo::default_plan() { return JWV_PLAN_REV_HEAD | JWV_PLAN_FWD_TAIL; }
 hipError_t launch_fwt_rev_head(const Bank& b, bool fma, const RevHeadArgs& a, hipStream_t s) {
   JWV_MODE2(fwt_rev_head, b, a, s);
 }

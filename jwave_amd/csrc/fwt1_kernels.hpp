@@ -35,41 +35,15 @@ struct Fwd1Geo {
   }
 };
 
-// Couple (pairs i, i+1) of fwd_pair with the tap loop shared: x[j] = window
-// sample 2i + j; the four sums keep fwd_pair's per-output order (j ascending
-// from +0.0) and are materialised after every tap, so the four dependent add
-// chains stay interleaved (the compiler otherwise runs two, each add waiting on
-// the multiply it consumes and on the previous add).
-template <int L, bool FMA>
-__device__ __forceinline__ void fwd_couple_ilv(const FwdTaps<L>& tp, const double* x, double& a0,
-                                               double& d0, double& a1, double& d1) {
-  double sa0 = 0.0, sd0 = 0.0, sa1 = 0.0, sd1 = 0.0;
-#pragma unroll
-  for (int j = 0; j < L; ++j) {
-    sa0 = mac<FMA>(sa0, x[j], FB<L>::lo(tp, j));
-    sd0 = mac<FMA>(sd0, x[j], FB<L>::hi(tp, j));
-    sa1 = mac<FMA>(sa1, x[j + 2], FB<L>::lo(tp, j));
-    sd1 = mac<FMA>(sd1, x[j + 2], FB<L>::hi(tp, j));
-    asm volatile("" : "+v"(sa0), "+v"(sd0), "+v"(sa1), "+v"(sd1));
-  }
-  a0 = sa0;
-  d0 = sd0;
-  a1 = sa1;
-  d1 = sd1;
-}
-
 #ifndef JWV_FWD_SLOT_FENCE
 #define JWV_FWD_SLOT_FENCE 1
 #endif
 #ifndef JWV_FWD_FENCE_MINL
 #define JWV_FWD_FENCE_MINL 12
 #endif
-// CP: a lane computes two adjacent pairs ("a couple", L+2 window values read
-// as 16-B LDS reads at a 32-B lane stride, 2-way bank-conflicted on
-// ds_read_b128); !CP: one pair per lane, L values read at a 16-B lane stride
-// (conflict-free), 8-B output stores.
-// CP = 2: couples with the four sums interleaved (fwd_couple_ilv).
-template <int L, int NT, int T, int K, bool FMA, int l, bool WT = false, int CP = 1>
+// A lane computes two adjacent pairs ("a couple", L+2 window values read as
+// 16-B LDS reads at a 32-B lane stride).
+template <int L, int NT, int T, int K, bool FMA, int l, bool WT = false>
 struct Fwd1Level {
   // level l reads the level-(l-1) window at lds + off(l-1) (l = 1: lds) and
   // writes its approximations at lds + off(l) (the last level: ya).
@@ -89,47 +63,6 @@ struct Fwd1Level {
     double* out = lds + G::off(l);
     const int tid = opaque_tid();  // per-level: keeps address math out of the prologue
     double* __restrict__ yd = yd0 + (hl >> 1) + (int64_t)t * own;
-    if constexpr (!CP) {
-      constexpr int RS = (mo + NT - 1) / NT;
-      double as[RS];
-#pragma unroll
-      for (int r = 0; r < RS; ++r) {
-        const int p = tid + r * NT;
-        if ((r + 1) * NT <= mo || p < mo) {
-          double x[L];
-#pragma unroll
-          for (int j = 0; j < L; j += 2) {
-            const double2 v = *reinterpret_cast<const double2*>(in + 2 * p + j);
-            x[j] = v.x;
-            x[j + 1] = v.y;
-          }
-          double a, d;
-          fwd_pair<L, FMA>(tp, [&](int j) { return x[j]; }, a, d);
-          if constexpr (l == K) {
-            if constexpr (WT) st_wt(ya + (int64_t)t * own + p, a);
-            else ya[(int64_t)t * own + p] = a;
-          } else if constexpr (l == 1) {
-            as[r] = a;
-          } else {
-            out[p] = a;
-          }
-          if (r * NT < own && ((r + 1) * NT <= own || p < own)) yd[p] = d;
-        }
-      }
-      if constexpr (l < K) {
-        if constexpr (l == 1) {
-          lds_barrier();
-#pragma unroll
-          for (int r = 0; r < RS; ++r) {
-            const int p = tid + r * NT;
-            if ((r + 1) * NT <= mo || p < mo) out[p] = as[r];
-          }
-        }
-        lds_barrier();
-        Fwd1Level<L, NT, T, K, FMA, l + 1, WT, CP>::run(tp, lds, yd0, hl >> 1, t, ya, sp);
-      }
-      return;
-    }
     double2 av[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -143,12 +76,8 @@ struct Fwd1Level {
           x[j + 1] = v.y;
         }
         double a0, d0, a1, d1;
-        if constexpr (CP == 2) {
-          fwd_couple_ilv<L, FMA>(tp, x, a0, d0, a1, d1);
-        } else {
-          fwd_pair<L, FMA>(tp, [&](int j) { return x[j]; }, a0, d0);
-          fwd_pair<L, FMA>(tp, [&](int j) { return x[j + 2]; }, a1, d1);
-        }
+        fwd_pair<L, FMA>(tp, [&](int j) { return x[j]; }, a0, d0);
+        fwd_pair<L, FMA>(tp, [&](int j) { return x[j + 2]; }, a1, d1);
         // long banks: a slot boundary keeps the compiler from hoisting every
         // slot's L+2 window reads at once (L = 16: 118 -> 54 VGPRs, 8 waves
         // per SIMD).  L = 8 (68 -> 40 VGPRs) measured 1.5% slower on config 2,
@@ -180,7 +109,7 @@ struct Fwd1Level {
         }
       }
       lds_barrier();
-      Fwd1Level<L, NT, T, K, FMA, l + 1, WT, CP>::run(tp, lds, yd0, hl >> 1, t, ya, sp);
+      Fwd1Level<L, NT, T, K, FMA, l + 1, WT>::run(tp, lds, yd0, hl >> 1, t, ya, sp);
     }
   }
 };
@@ -188,7 +117,7 @@ struct Fwd1Level {
 // Grid: nouter * (h / T) blocks, tile-fastest, XCD-remapped like fwt_fwd_tile.
 // src: level input (length h, stride 1); dst: coefficient array of the
 // signal (details of level size hl at dst[hl/2 ..]); adst: level-K output.
-template <int L, int NT, int T, int K, bool FMA, int CP = 1>
+template <int L, int NT, int T, int K, bool FMA>
 __global__ __launch_bounds__(NT) void fwt_fwd_tile1(const double* __restrict__ src,
                                                     int64_t s_src, double* __restrict__ dst,
                                                     int64_t s_dst, double* __restrict__ adst,
@@ -208,7 +137,7 @@ __global__ __launch_bounds__(NT) void fwt_fwd_tile1(const double* __restrict__ s
                                           [&](int e) { return (int64_t)((base + e) & msk); });
   dma_fence_barrier();
   JWV_STAMP(1);
-  Fwd1Level<L, NT, T, K, FMA, 1, false, CP>::run(tp, lds, dst + o * s_dst, h, t, adst + o * s_adst,
+  Fwd1Level<L, NT, T, K, FMA, 1, false>::run(tp, lds, dst + o * s_dst, h, t, adst + o * s_adst,
                                                  sp);
 }
 

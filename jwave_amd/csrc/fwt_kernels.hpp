@@ -454,112 +454,6 @@ __global__ __launch_bounds__(NT) void fwt_fwd_tile(const double* __restrict__ sr
   }
 }
 
-// ====================================================================
-// Forward, streaming (C = 1 hot path: long 1-D signals, batches of them).
-// Persistent blocks of NTC compute threads + 1 loader wave.  The loader wave
-// keeps one tile ahead: while the compute waves run the K fused levels of
-// tile i out of LDS buffer i&1, it LDS-DMAs tile i+1's window into the other
-// buffer, so the CU's HBM stream never pauses for compute (a plain one-tile
-// block loads, then computes, with its co-resident blocks in the same phase).
-// The loader joins every block barrier and never stores, so its own
-// `s_waitcnt vmcnt(0)` waits for its DMA only.  Tile order is XCD-aware: the
-// blocks of one XCD walk a contiguous chunk of tiles side by side, so a
-// tile's halo is its neighbour's head, already in that XCD's L2.
-// Math and outputs are identical to fwt_fwd_tile.
-// ====================================================================
-template <int L, int NTC, int T, int KMAX, bool FMA>
-__global__ __launch_bounds__(NTC + 64) void fwt_fwd_stream(
-    const double* __restrict__ src, AxisView sv, double* __restrict__ dst, AxisView dv,
-    double* __restrict__ adst, AxisView av_, int h, int K, int64_t ntotal,
-    typename FB<L>::Fwd tp) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  constexpr int LM = LMax<L>::v;
-  constexpr int M0MAX = T + (LM - 2) * ((1 << KMAX) - 1);
-  constexpr int WBUF = (M0MAX + 3) & ~1;  // + DMA overrun, even
-  constexpr int MAXP = ((M0MAX - (LM - 2)) / 2 + NTC - 1) / NTC;
-  const int nL = FB<L>::n(tp);
-  const int ntile = h / T;
-  const int tid = threadIdx.x;
-  const bool loader = tid >= NTC;
-  const int lane = tid & 63;
-  const int m0 = T + (nL - 2) * ((1 << K) - 1);
-  const int msk = h - 1;
-  const int nunits = (m0 + 1) >> 1;
-
-  // XCD-aware tile walk: block b sits on XCD b%8 (speed only, not correctness)
-  const int64_t nb = gridDim.x;
-  const int64_t b = blockIdx.x;
-  int64_t first, stride, count;
-  if ((nb & 7) == 0 && (ntotal & 7) == 0) {
-    const int64_t nper = nb >> 3, chunk = ntotal >> 3;
-    const int64_t x = b & 7, slot = b >> 3;
-    first = x * chunk + slot;
-    stride = nper;
-    count = slot < chunk ? (chunk - slot + nper - 1) / nper : 0;
-  } else {
-    first = b;
-    stride = nb;
-    count = b < ntotal ? (ntotal - b + nb - 1) / nb : 0;
-  }
-
-  auto issue = [&](int64_t g, double* buf) {  // loader wave only
-    const int64_t o = g / ntile;
-    const int t = (int)(g % ntile);
-    const double* s = src + view_base(sv, o);
-    const int base = t * T;
-    for (int u0 = 0; u0 < nunits; u0 += 64) {
-      const int u = u0 + lane;
-      if (u < nunits) dma16_asm((const void*)(s + ((base + 2 * u) & msk)), buf + 2 * u0);
-    }
-  };
-
-  if (loader && count > 0) issue(first, lds);
-  if (loader) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  lds_barrier();
-
-  for (int64_t k = 0; k < count; ++k) {
-    const int64_t g = first + k * stride;
-    double* cur = lds + (k & 1) * WBUF;
-    if (k < 10) JWV_STAMP(3 * k);
-    if (loader && k + 1 < count) issue(g + stride, lds + ((k + 1) & 1) * WBUF);
-    const int64_t o = g / ntile;
-    const int t = (int)(g % ntile);
-    double* y = dst + view_base(dv, o);
-    double* ya = adst + view_base(av_, o);
-    int m = m0, hl = h;
-    for (int l = 1; l <= K; ++l) {
-      const int mo = (m - (nL - 2)) >> 1;
-      const int own = T >> l;
-      const int64_t dbase = (int64_t)(hl >> 1) + (int64_t)t * own;
-      double av[MAXP];
-      if (!loader) {
-        for_pairs<MAXP, NTC>(mo, [&](int r, int p, bool v) {
-          double a, d;
-          fwd_pair<L, FMA>(tp, [&](int j) { return cur[2 * p + j]; }, a, d);
-          av[r] = a;
-          if (v && p < own) y[dbase + p] = d;
-        });
-      }
-      lds_barrier();
-      if (!loader) {
-        for_pairs<MAXP, NTC>(mo, [&](int r, int p, bool v) {
-          if (v) cur[p] = av[r];
-        });
-      }
-      lds_barrier();
-      m = mo;
-      hl >>= 1;
-    }
-    const int own = T >> K;
-    if (!loader)
-      for (int q = tid; q < own; q += NTC) ya[(int64_t)t * own + q] = cur[q];
-    if (k < 10) JWV_STAMP(3 * k + 1);
-    if (loader) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_barrier();  // next buffer landed; this buffer free for the tile after
-    if (k < 10) JWV_STAMP(3 * k + 2);
-  }
-}
-
 // One synthesis pair at global pair index m (m < qe-1: array head, whose
 // terms are summed in scatter order by rev_pair_head).  A/D point at the LDS
 // copies of a[m], d[m] (stride C); Aw(q)/Dw(q) give a[m-q]/d[m-q] wrapped.

@@ -80,38 +80,29 @@ struct Geo {
   static constexpr int kWptT8 = 512, kWptK8 = 3;
   static constexpr int kModT = 4096, kModTInv = 1024, kModS = 2048;
   static int res_cap(int C) { return C == 1 ? kResCap1 : kResCap8; }
-  // tile of the C = 1 FWT passes: 4096 (default) or 2048, env JWV_FWD_T / JWV_REV_T;
-  // reverse detail prefetch-all: env JWV_REV_PREF=1
+  // tile of the C = 1 FWT passes (4096)
   static int fwd_t1();
   static int rev_t1();
-  static bool rev_pref();
-  static bool fwd_stream();          // env JWV_FWD_STREAM (default 0)
-  static int stream_blocks_per_cu(); // env JWV_STREAM_BPC (default 2)
-  static int stream_ntc();           // env JWV_STREAM_NTC: 256 | 512 (default 512)
+  static bool rev_pref();  // reverse detail prefetch-all (off)
   // C = 1 compile-time-geometry kernels (fwt1_kernels.hpp, fwt1_res.hpp):
-  // env JWV_FWT1 (default 1).  Tiles: forward T = 4096, reverse T = 2048, up
+  // on.  Tiles: forward T = 4096, reverse T = 2048, up
   // to kFwt1KMax fused levels; the planner lets the last forward tile pass run
   // down to kFwt1Tail samples and starts the reverse tile passes above
   // kFwt1Tail * 2, so the single-block tails stay short.
   static bool fwt1();
-  // C = 8 compile-time-geometry column-slab tiles (fwt8_kernels.hpp): env
-  // JWV_FWT8 (default 1)
+  // C = 8 compile-time-geometry column-slab tiles (fwt8_kernels.hpp): on
   static bool fwt8();
-  // block order of the C = 8 slab tiles: 0 tile-fastest, 1 slab-fastest
-  // (env JWV_SLAB_ORDER)
+  // block order of the C = 8 slab tiles: 1 slab-fastest
   static int slab_order();
-  // st2_pol policy of the passes that write the full-length output (forward:
-  // the first tile pass's details; reverse: the last tile pass): env
-  // JWV_STPOL (0 plain, 1 sc1, 2 nt)
+  // st2_pol policy of the full-length output passes (0 plain)
   static int store_pol();
-  static int tile_desc(int rev);  // sp bit 2 for the big pass (env JWV_TILE_DESC)
+  static int tile_desc(int rev);  // sp bit 2 for the big pass (0)
   // sp bits of the C = 1 tile walk (tile_order): the grouped one-front walk
-  // with G = 64 tiles per XCD group (env JWV_TILE_G = G, a power of two;
-  // 0 = the XCD-chunked walk)
+  // with G = 64 tiles per XCD group
   static int tile_walk();
   // First (full-length) forward pass of one long contiguous signal: tile
-  // (2048 | 1024, env JWV_FWD1T) and fused levels (env JWV_FWD1K); the last
-  // forward tile pass runs down to fwd1_tail() samples (env JWV_FWD1TAIL).
+  // and fused levels; the last forward tile pass runs down to fwd1_tail()
+  // samples.
   static int fwd1_first_t();
   static int fwd1_first_k();
   static int fwd1_tail();
@@ -132,7 +123,7 @@ struct ChainGeo {
   static constexpr int kTA = 2048;
   static constexpr int kTM = 2048, kKM = 9, kKAr = 5;
   static constexpr int kWords = 4096;  // sync words per direction (ctx buffer: 2x)
-  static int default_plan();          // JWV_PLAN_* bits: env JWV_PLAN, default REV_HEAD
+  static int default_plan();          // JWV_PLAN_* bits: REV_HEAD | FWD_TAIL
 };
 struct ChainFwdArgs {
   const double* src; double* dst;

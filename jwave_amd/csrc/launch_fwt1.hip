@@ -31,19 +31,9 @@ hipError_t prep1(Kern kernel, size_t lds) {
   return hipSuccess;
 }
 
-// env JWV_FWD1CP (default 1): 0 = one pair per lane in the full-length
-// forward pass (conflict-free 16-B LDS reads) instead of couples; 2 = couples
-// with the four sums interleaved (fwd_couple_ilv)
-int fwd1_couples() {
-  static const int v = [] {
-    const char* e = std::getenv("JWV_FWD1CP");
-    return e ? std::atoi(e) : 1;
-  }();
-  return v;
-}
-template <int L, int NT, int T, int K, int CP = 1>
+template <int L, int NT, int T, int K>
 hipError_t fwd1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
-  auto k = fwt_fwd_tile1<L, NT, T, K, kFMA, CP>;
+  auto k = fwt_fwd_tile1<L, NT, T, K, kFMA>;
   const size_t lds = (size_t)Fwd1Geo<L, T, K>::lds_doubles() * sizeof(double);
   if (hipError_t e = prep1(k, lds)) return e;
   FwdTaps<L> tp;
@@ -70,10 +60,7 @@ hipError_t fwd1_l(const Bank& b, const TileArgs& a, hipStream_t s) {
     case 3: return fwd1_k<L, NT, T, 3>(b, a, s);
     case 4: return fwd1_k<L, NT, T, 4>(b, a, s);
     case 5: return fwd1_k<L, NT, T, 5>(b, a, s);
-    case 6:
-      if (L <= 8 && fwd1_couples() == 0) return fwd1_k<L, NT, T, 6, 0>(b, a, s);
-      if (L <= 8 && fwd1_couples() == 2) return fwd1_k<L, NT, T, 6, 2>(b, a, s);
-      return fwd1_k<L, NT, T, 6>(b, a, s);
+    case 6: return fwd1_k<L, NT, T, 6>(b, a, s);
     // deep passes (latency-bound, few blocks): 512 threads halve the pair
     // slots of the wide levels (config 2: 0.6 us per call)
     case 7: return fwd1_k<L, 512, T, 7>(b, a, s);
@@ -171,26 +158,14 @@ bool fwt_fwd_tile1(const Bank& b, const TileArgs& a, hipStream_t s, hipError_t& 
 // A handful of signals (the latency-bound tail of long 1-D signals): 1024
 // threads; batches of rows up to kRowCap: 256 threads (res1_rows).
 // Batches of short rows (<= kRowCap) also take the compiled-in kernels with
-// 256 threads (env JWV_RES1ROWS=0: the generic ones).  Config 3 row tails:
+// 256 threads.  Config 3 row tails:
 // fwd 51 -> 41 us, rev ~100 -> 90 us.
-bool res1_rows() {
-  static const bool v = [] {
-    const char* e = std::getenv("JWV_RES1ROWS");
-    return e ? std::atoi(e) != 0 : true;
-  }();
-  return v;
-}
+bool res1_rows() { return true; }
 // Batches of >= 64 rows up to kSmallH samples (the row passes' resident
-// tails, config 3): one wave per row (fwt1_row.hpp), env JWV_SMALL1=0: the
+// tails, config 3): one wave per row (fwt1_row.hpp) instead of the
 // block-per-row kernels above.  Config 3 tails (8192 rows, one box):
 // forward 45.8 -> 40.1 us, reverse 79.0 -> 73.9 us.
-bool small1() {
-  static const bool v = [] {
-    const char* e = std::getenv("JWV_SMALL1");
-    return e ? std::atoi(e) != 0 : true;
-  }();
-  return v;
-}
+bool small1() { return true; }
 template <int L>
 hipError_t fwd_small1_l(const Bank& b, const ResArgs& a, hipStream_t s) {
   FwdTaps<L> tp;

@@ -126,43 +126,8 @@ hipError_t fwt_fwd_tile_t(const Bank& b, const TileArgs& a, hipStream_t s) {
                      a.inner, a.dma, fwd_taps<L>(b));
   return hipGetLastError();
 }
-// Streaming forward (C = 1, contiguous aligned signals): persistent blocks.
-template <int L, int T, int NTC>
-hipError_t fwt_fwd_stream_t(const Bank& b, const TileArgs& a, hipStream_t s) {
-  constexpr int KM = Geo::kFwtK1;
-  auto k = fwt_fwd_stream<L, NTC, T, KM, kFMA>;
-  constexpr int LM = LMax<L>::v;
-  constexpr int M0MAX = T + (LM - 2) * ((1 << KM) - 1);
-  constexpr int WBUF = (M0MAX + 3) & ~1;
-  const size_t lds = (size_t)2 * WBUF * sizeof(double);
-  if (hipError_t e = prep(k, lds)) return e;
-  const int64_t ntotal = a.nouter * (int64_t)(a.h / T);
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        ncu <= 0)
-      ncu = 256;
-  }
-  const int per_cu = Geo::stream_blocks_per_cu();
-  int64_t grid = (int64_t)ncu * per_cu;
-  if (grid > ntotal) grid = ((ntotal + 7) / 8) * 8;
-  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(NTC + 64), lds, s, a.src, a.sv, a.dst, a.dv,
-                     a.adst, a.av, a.h, a.K, ntotal, fwd_taps<L>(b));
-  return hipGetLastError();
-}
 template <int L, int C>
 hipError_t fwt_fwd_tile_go(const Bank& b, const TileArgs& a, hipStream_t s) {
-  if constexpr (C == 1) {
-    if (a.dma && Geo::fwd_stream()) {
-      const bool w = Geo::stream_ntc() == 512;
-      if (Geo::fwd_t1() == 2048)
-        return w ? fwt_fwd_stream_t<L, 2048, 512>(b, a, s) : fwt_fwd_stream_t<L, 2048, 256>(b, a, s);
-      return w ? fwt_fwd_stream_t<L, 4096, 512>(b, a, s) : fwt_fwd_stream_t<L, 4096, 256>(b, a, s);
-    }
-    if (Geo::fwd_t1() == 2048) return fwt_fwd_tile_t<L, C, 2048>(b, a, s);
-  }
   return fwt_fwd_tile_t<L, C, fwt_T<C>()>(b, a, s);
 }
 template <int L, int C, int T, bool PREF>
@@ -182,13 +147,6 @@ hipError_t fwt_rev_tile_t(const Bank& b, const TileArgs& a, hipStream_t s) {
 }
 template <int L, int C>
 hipError_t fwt_rev_tile_go(const Bank& b, const TileArgs& a, hipStream_t s) {
-  if constexpr (C == 1) {
-    const bool pref = Geo::rev_pref();
-    if (Geo::rev_t1() == 2048)
-      return pref ? fwt_rev_tile_t<L, C, 2048, true>(b, a, s)
-                  : fwt_rev_tile_t<L, C, 2048, false>(b, a, s);
-    if (pref) return fwt_rev_tile_t<L, C, fwt_T<C>(), true>(b, a, s);
-  }
   return fwt_rev_tile_t<L, C, fwt_T<C>(), false>(b, a, s);
 }
 

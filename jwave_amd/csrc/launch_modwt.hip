@@ -45,20 +45,10 @@ unsigned level_grid(int64_t N) {
   return (unsigned)(g < 8192 ? (g > 0 ? g : 1) : 8192);
 }
 
-// Tile geometry variants (NT threads, T outputs per block): env JWV_MODFWD /
-// JWV_MODINV select one.  Larger tiles cut the halo recompute
-// (the right/left halo is (L-1)(2^j1 - 2^(j0-1)), 1785 samples for D4 J=8).
-int env_variant(const char* name) {
-  const char* v = std::getenv(name);
-  return v ? std::atoi(v) : -1;
-}
-// Defaults measured on config 5 (D4, J=8, N=1e7): fwd 1 (512 x 4096) 228 ->
-// 203 us, inv 2 (512 x 2048) 386 -> 300 us, inv 10 (class-major layout, 512 x
-// 2048) 300 -> 285 us.  The register-blocked (3-6) and two-deep prefetch
-// (7-9) variants measured no better and stay selectable.
-int fwd_variant() { static const int v = env_variant("JWV_MODFWD"); return v < 0 ? 1 : v; }
-int inv_variant() { static const int v = env_variant("JWV_MODINV"); return v < 0 ? 10 : v; }
-
+// Runtime-geometry tiles (banks the compile-time kernels do not cover):
+// forward 512 x 4096 (config 5 228 -> 203 us against 256 x 1024), inverse in
+// the class-major layout, 512 x 2048 (386 -> 285 us); register-blocked and
+// two-deep-prefetch variants measured no better and were removed.
 template <int L, int NTX, int TX>
 hipError_t fwd_tile_go(const Bank& b, const ModwtArgs& a, hipStream_t s) {
   const auto tp = mtaps<L>(b);
@@ -72,33 +62,10 @@ hipError_t fwd_tile_go(const Bank& b, const ModwtArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int L, int NTX, int TX, int KO>
-hipError_t fwd_tile_g_go(const Bank& b, const ModwtArgs& a, hipStream_t s) {
-  if constexpr (L == 0) {
-    return fwd_tile_go<L, NT, T>(b, a, s);
-  } else {
-    const auto tp = mtaps<L>(b);
-    auto k = modwt_fwd_tile_g<L, NTX, TX, SMAX, KO, kFMA>;
-    const int S = (b.L - 1) * ((1 << a.j1) - (1 << (a.j0 - 1)));
-    const size_t lds = (size_t)(TX + S) * sizeof(double);
-    if (hipError_t e = prep(k, lds)) return e;
-    const dim3 grid((unsigned)((a.N + TX - 1) / TX));
-    hipLaunchKernelGGL(k, grid, dim3(NTX), lds, s, a.src, a.wout, a.ldw, a.vout, a.N, a.j0,
-                       a.j1, tp);
-    return hipGetLastError();
-  }
-}
-
 template <int L>
 hipError_t fwd_go(const Bank& b, bool tiled, const ModwtArgs& a, hipStream_t s) {
   if (tiled) {
-    switch (fwd_variant()) {
-      case 1: return fwd_tile_go<L, 512, 4096>(b, a, s);
-      case 2: return fwd_tile_go<L, 1024, 8192>(b, a, s);
-      case 3: return fwd_tile_g_go<L, 512, 4096, 4>(b, a, s);
-      case 4: return fwd_tile_g_go<L, 256, 4096, 4>(b, a, s);
-      default: return fwd_tile_go<L, NT, T>(b, a, s);
-    }
+    return fwd_tile_go<L, 512, 4096>(b, a, s);
   }
   const auto tp = mtaps<L>(b);
   auto k = modwt_fwd_level<L, kFMA>;
@@ -121,36 +88,6 @@ hipError_t inv_tile_go(const Bank& b, const ModwtArgs& a, hipStream_t s) {
 }
 
 template <int L, int NTX, int TX>
-hipError_t inv_tile2_go(const Bank& b, const ModwtArgs& a, hipStream_t s) {
-  const auto tp = mtaps<L>(b);
-  auto k = modwt_inv_tile2<L, NTX, TX, SMAX, kFMA>;
-  const int R = (b.L - 1) * ((1 << a.j1) - (1 << (a.j0 - 1)));
-  const size_t lds = (size_t)2 * (TX + R) * sizeof(double);
-  if (hipError_t e = prep(k, lds)) return e;
-  const dim3 grid((unsigned)((a.N + TX - 1) / TX));
-  hipLaunchKernelGGL(k, grid, dim3(NTX), lds, s, a.src, a.coef, a.ldw, a.vout, a.N, a.j0, a.j1,
-                     tp);
-  return hipGetLastError();
-}
-
-template <int L, int NTX, int TX, int KO>
-hipError_t inv_tile_g_go(const Bank& b, const ModwtArgs& a, hipStream_t s) {
-  if constexpr (L == 0) {
-    return inv_tile_go<L, NT, TI>(b, a, s);
-  } else {
-    const auto tp = mtaps<L>(b);
-    auto k = modwt_inv_tile_g<L, NTX, TX, SMAX, KO, kFMA>;
-    const int R = (b.L - 1) * ((1 << a.j1) - (1 << (a.j0 - 1)));
-    const size_t lds = (size_t)2 * (TX + R) * sizeof(double);
-    if (hipError_t e = prep(k, lds)) return e;
-    const dim3 grid((unsigned)((a.N + TX - 1) / TX));
-    hipLaunchKernelGGL(k, grid, dim3(NTX), lds, s, a.src, a.coef, a.ldw, a.vout, a.N, a.j0,
-                       a.j1, tp);
-    return hipGetLastError();
-  }
-}
-
-template <int L, int NTX, int TX>
 hipError_t inv_tile_cm_go(const Bank& b, const ModwtArgs& a, hipStream_t s) {
   if constexpr (L == 0) {
     return inv_tile_go<L, NT, TI>(b, a, s);
@@ -170,19 +107,7 @@ hipError_t inv_tile_cm_go(const Bank& b, const ModwtArgs& a, hipStream_t s) {
 template <int L>
 hipError_t inv_go(const Bank& b, bool tiled, const ModwtArgs& a, hipStream_t s) {
   if (tiled) {
-    switch (inv_variant()) {
-      case 1: return inv_tile_go<L, 1024, 4096>(b, a, s);
-      case 2: return inv_tile_go<L, 512, 2048>(b, a, s);
-      case 3: return inv_tile_go<L, 512, 4096>(b, a, s);
-      case 4: return inv_tile_g_go<L, 512, 2048, 4>(b, a, s);
-      case 5: return inv_tile_g_go<L, 256, 2048, 4>(b, a, s);
-      case 6: return inv_tile_g_go<L, 512, 4096, 4>(b, a, s);
-      case 7: return inv_tile2_go<L, 512, 2048>(b, a, s);
-      case 8: return inv_tile2_go<L, 256, 1024>(b, a, s);
-      case 9: return inv_tile2_go<L, 1024, 4096>(b, a, s);
-      case 10: return inv_tile_cm_go<L, 512, 2048>(b, a, s);
-      default: return inv_tile_go<L, NT, TI>(b, a, s);
-    }
+    return inv_tile_cm_go<L, 512, 2048>(b, a, s);
   }
   const auto tp = mtaps<L>(b);
   auto k = modwt_inv_level<L, kFMA>;

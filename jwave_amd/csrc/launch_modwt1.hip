@@ -1,9 +1,10 @@
-// launch_modwt1.hip — the compile-time-geometry MODWT tiles
-// (modwt1_kernels.hpp) for one math mode (compiled twice, like
+// launch_modwt1.hip — the compile-time-geometry MODWT kernels (modwt_pipe.hpp,
+// modwt1_kernels.hpp) for one math mode (compiled twice, like
 // launch_modwt.hip).  Covered: tap count L = 8, fused levels 1..j1 with
 // j1 <= 8 (config 5: Daubechies4, J = 8, one launch per direction); every
 // other case keeps the runtime-geometry tiles.
 #include "modwt1_kernels.hpp"
+#include "modwt_pipe.hpp"
 #include "jwv_modwt1.hpp"
 
 #include <cstdlib>
@@ -35,38 +36,6 @@ ModwtTaps<L> taps(const Bank& b) {
   for (int j = 0; j < L; ++j) { t.g[j] = b.lo[j]; t.h[j] = b.hi[j]; }
   return t;
 }
-
-// env JWV_MODWT_P2 (default 3): bit 0 forward, bit 1 inverse — two adjacent
-// outputs per lane (16-B LDS reads); a clear bit = one output per lane
-int p2_bits() {
-  static const int v = [] {
-    const char* e = std::getenv("JWV_MODWT_P2");
-    return e ? std::atoi(e) : 3;
-  }();
-  return v;
-}
-
-template <int L, int J1, bool P2, int NT = kNT, int TF = kTF, int M = 1>
-hipError_t fwd_kp(const Bank& b, const ModwtArgs& a, hipStream_t s) {
-  auto k = modwt_fwd_tile1<L, NT, TF, 1, J1, kFMA, P2, M>;
-  const size_t lds = (size_t)ModFwd1Geo<L, TF, 1, J1>::lds_doubles(M) * sizeof(double);
-  if (hipError_t e = prep(k, lds)) return e;
-  const dim3 grid((unsigned)((a.N + TF - 1) / TF));
-  hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.wout, a.ldw, a.vout, a.N, taps<L>(b));
-  return hipGetLastError();
-}
-// Persistent tiles (modwt_fwd_tile1p / modwt_inv_tile1p): blocks per CU x
-// CUs, a multiple of 8 (XCDs); env JWV_MODWT_PF bit 0 forward, bit 1 inverse
-// (a clear bit keeps the one-tile-per-block grid).  Off by default: r03, one
-// box, two rounds: forward 169.2 / 169.6 us one tile per block vs 200.3 /
-// 201.3 persistent; inverse (303) 225.0 / 226.8 vs 243.2 / 246.6.
-int pf_env() {
-  static const int v = [] {
-    const char* e = std::getenv("JWV_MODWT_PF");
-    return e ? std::atoi(e) : 0;
-  }();
-  return v;
-}
 int cu_count() {
   static const int v = [] {
     int dev = 0, n = 0;
@@ -77,125 +46,127 @@ int cu_count() {
   }();
   return v;
 }
-template <int L, int J1, int NT, int TF, int M = 1>
-hipError_t fwd_kpp(const Bank& b, const ModwtArgs& a, hipStream_t s) {
-  auto k = modwt_fwd_tile1p<L, NT, TF, 1, J1, kFMA, true, M>;
-  const size_t lds = (size_t)ModFwd1Geo<L, TF, 1, J1>::lds_doubles(M) * sizeof(double);
+
+// One tile per block (modwt1_kernels.hpp): the fallback of the pipelined
+// kernels for rows or outputs that are not 16-B aligned.  Two outputs per
+// lane (P2).  Full depth (J1 = 8, config 5): forward 1024 x 8192 tiles (half
+// the halo recompute of 4096-sample tiles; 512 x 8192: 200 us, 256 x 4096:
+// 214 us, against 173-176), inverse 512 x 2048 in the run form from level 3
+// (M = 303: 235 us against 250 for P2 on every level).
+template <int L, int J1, int NT, int TF>
+hipError_t fwd_kp(const Bank& b, const ModwtArgs& a, hipStream_t s) {
+  auto k = modwt_fwd_tile1<L, NT, TF, 1, J1, kFMA, true, 1>;
+  const size_t lds = (size_t)ModFwd1Geo<L, TF, 1, J1>::lds_doubles(1) * sizeof(double);
   if (hipError_t e = prep(k, lds)) return e;
-  const int64_t ntile = (a.N + TF - 1) / TF;
-  const int per_cu = lds > 81920 ? 1 : 2;
-  int64_t nb = (int64_t)(cu_count() / 8) * per_cu;  // blocks per XCD
-  const int64_t need = (ntile + 7) / 8;            // tiles per XCD chunk
-  if (nb > need) nb = need;
-  if (nb < 1) nb = 1;
-  hipLaunchKernelGGL(k, dim3((unsigned)(8 * nb)), dim3(NT), lds, s, a.src, a.wout, a.ldw, a.vout,
-                     a.N, taps<L>(b));
+  const dim3 grid((unsigned)((a.N + TF - 1) / TF));
+  hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.wout, a.ldw, a.vout, a.N, taps<L>(b));
   return hipGetLastError();
 }
-template <int L, int J1, int NT, int TI, int M = 1>
-hipError_t inv_kpp(const Bank& b, const ModwtArgs& a, hipStream_t s) {
-  auto k = modwt_inv_tile1p<L, NT, TI, 1, J1, kFMA, true, M>;
-  const size_t lds = (size_t)ModInv1Geo<L, TI, 1, J1>::lds_doubles(M) * sizeof(double);
-  if (hipError_t e = prep(k, lds)) return e;
-  const int64_t ntile = (a.N + TI - 1) / TI;
-  const int per_cu = (int)(163840 / (lds + 1024));  // LDS-bound blocks per CU
-  int64_t nb = (int64_t)(cu_count() / 8) * (per_cu < 1 ? 1 : per_cu);
-  const int64_t need = (ntile + 7) / 8;
-  if (nb > need) nb = need;
-  if (nb < 1) nb = 1;
-  hipLaunchKernelGGL(k, dim3((unsigned)(8 * nb)), dim3(NT), lds, s, a.src, a.coef, a.ldw, a.vout,
-                     a.N, taps<L>(b));
-  return hipGetLastError();
-}
-// tile geometry of the full-depth (J1 = 8) launches: env JWV_MODWT_GF (forward)
-// / JWV_MODWT_GI (inverse) = 0 default, 1.. the alternatives below
-int geo_env(const char* name) {
-  const char* e = std::getenv(name);
-  return e ? std::atoi(e) : 0;
-}
-int geo_f() { static const int v = geo_env("JWV_MODWT_GF"); return v; }
-// Run form (ModRun) of the full-depth launches: env JWV_MODWT_RUN (inverse) /
-// JWV_MODWT_RUNF (forward) = m + 100*jr, m pairs per lane on levels j >= jr
-// (3, 303, 503; 1 = the two-output P2 form on every level)
-int run_env(const char* name, int dflt) {
-  const char* e = std::getenv(name);
-  return e ? std::atoi(e) : dflt;
-}
-// inverse: 303 (r03, one box, two rounds: 235.3 / 236.8 us against 250.0 /
-// 252.1 for the P2 form, 243.5 / 239.7 for 3, 239.1 / 237.9 for 503)
-int run_m() { static const int v = run_env("JWV_MODWT_RUN", 303); return v; }
-// forward (env JWV_MODWT_RUNF): 1, the P2 form (r03: 176.3 / 174.4 us against
-// 207.9 / 209.4 for 3, 203.6 / 203.0 for 303, 206.0 / 205.1 for 503 — the run
-// form's W stores leave the wave as H-slot runs M*H slots apart)
-int run_f() { static const int v = run_env("JWV_MODWT_RUNF", 1); return v; }
-int geo_i() { static const int v = geo_env("JWV_MODWT_GI"); return v; }
-template <int L, int J1, bool P2, int NT = kNT, int TI = kTI, int M = 1>
+template <int L, int J1, int M>
 hipError_t inv_kp(const Bank& b, const ModwtArgs& a, hipStream_t s) {
-  auto k = modwt_inv_tile1<L, NT, TI, 1, J1, kFMA, P2, M>;
-  const size_t lds = (size_t)ModInv1Geo<L, TI, 1, J1>::lds_doubles(M) * sizeof(double);
+  auto k = modwt_inv_tile1<L, kNT, kTI, 1, J1, kFMA, true, M>;
+  const size_t lds = (size_t)ModInv1Geo<L, kTI, 1, J1>::lds_doubles(M) * sizeof(double);
   if (hipError_t e = prep(k, lds)) return e;
-  const dim3 grid((unsigned)((a.N + TI - 1) / TI));
-  hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.coef, a.ldw, a.vout, a.N, taps<L>(b));
+  const dim3 grid((unsigned)((a.N + kTI - 1) / kTI));
+  hipLaunchKernelGGL(k, grid, dim3(kNT), lds, s, a.src, a.coef, a.ldw, a.vout, a.N, taps<L>(b));
   return hipGetLastError();
 }
-// Full-depth forward (J1 = 8, config 5): 1024 x 8192 tiles (half the halo
-// recompute of 4096-sample tiles; 16 waves per CU either way): 186-188 ->
-// 173-176 us per launch (two runs, one box); 512 x 8192 (200 us) and
-// 256 x 4096 (214 us) measured slower.  JWV_MODWT_GF selects the others.
+
+// Pipelined inverse / forward (modwt_pipe.hpp): persistent 1024-thread blocks,
+// one per CU, windows by LDS-DMA; tiles 1024 (inverse) / 8192 (forward).
+// Need 16-B aligned rows (ldw even) and outputs.  env JWV_MODWT_PIPE: bit 0
+// inverse, bit 1 forward (default 3).
+constexpr int kPipeT = 1024, kPipeNT = 1024, kPipeTF = 8192;
+int pipe_env() {
+  static const int v = [] {
+    const char* e = std::getenv("JWV_MODWT_PIPE");
+    return e ? std::atoi(e) : 3;
+  }();
+  return v;
+}
+template <int L, int J1>
+bool fwd_pipe(const Bank& b, const ModwtArgs& a, hipStream_t s, hipError_t& err) {
+  using G = FwdPipeGeo<L, kPipeTF, J1>;
+  if (!(pipe_env() & 2) || (a.ldw & 1) ||
+      (((uintptr_t)a.wout | (uintptr_t)a.src | (uintptr_t)a.vout) & 15))
+    return false;
+  const size_t lds = (size_t)G::lds_doubles() * sizeof(double);
+  static_assert(G::lds_doubles() * 8 <= 163840, "pipe LDS");
+  const int64_t ntile = (a.N + kPipeTF - 1) / kPipeTF;
+  int64_t ti0 = (G::S + (G::S & 1) + kPipeTF - 1) / kPipeTF;
+  int64_t ti1 = a.N / kPipeTF;
+  if (ti1 < ti0) ti1 = ti0 = 0;  // no interior tile: every tile takes the edge kernel
+  const ModwtTaps<L> tp = taps<L>(b);
+  if (ti1 > ti0) {
+    auto k = modwt_fwd_pipe<L, kPipeNT, kPipeTF, J1, kFMA>;
+    if ((err = prep(k, lds))) return true;
+    int64_t per = cu_count() / 8;
+    const int64_t need = (ti1 - ti0 + 7) / 8;
+    if (per > need) per = need;
+    if (per < 1) per = 1;
+    hipLaunchKernelGGL(k, dim3((unsigned)(8 * per)), dim3(kPipeNT), lds, s, a.src, a.wout, a.ldw,
+                       a.vout, a.N, ti0, ti1, tp);
+    if ((err = hipGetLastError())) return true;
+  }
+  const int64_t nedge = ti0 + (ntile - ti1);
+  if (nedge > 0) {
+    auto k = modwt_fwd_pipe_edge<L, kPipeNT, kPipeTF, J1, kFMA>;
+    if ((err = prep(k, lds))) return true;
+    hipLaunchKernelGGL(k, dim3((unsigned)nedge), dim3(kPipeNT), lds, s, a.src, a.wout, a.ldw,
+                       a.vout, a.N, ti0, ti1, tp);
+    err = hipGetLastError();
+  }
+  return true;
+}
+template <int L, int J1>
+bool inv_pipe(const Bank& b, const ModwtArgs& a, hipStream_t s, hipError_t& err) {
+  if constexpr (J1 < 2) {
+    return false;
+  } else {
+    using G = InvPipeGeo<L, kPipeT, J1>;
+    if (!(pipe_env() & 1) || (a.ldw & 1) ||
+        (((uintptr_t)a.coef | (uintptr_t)a.src | (uintptr_t)a.vout) & 15))
+      return false;
+    const size_t lds = (size_t)G::lds_doubles() * sizeof(double);
+    static_assert(G::lds_doubles() * 8 <= 163840, "pipe LDS");
+    const int64_t u2 = 2 * G::units(J1);
+    const int64_t ntile = (a.N + kPipeT - 1) / kPipeT;
+    const int64_t ninner = a.N >= u2 ? (a.N - u2) / kPipeT + 1 : 0;
+    const ModwtTaps<L> tp = taps<L>(b);
+    if (ninner > 0) {
+      auto k = modwt_inv_pipe<L, kPipeNT, kPipeT, J1, kFMA>;
+      if ((err = prep(k, lds))) return true;
+      int64_t per = cu_count() / 8;
+      const int64_t need = (ninner + 7) / 8;
+      if (per > need) per = need;
+      if (per < 1) per = 1;
+      hipLaunchKernelGGL(k, dim3((unsigned)(8 * per)), dim3(kPipeNT), lds, s, a.src, a.coef, a.ldw,
+                         a.vout, a.N, ninner, tp);
+      if ((err = hipGetLastError())) return true;
+    }
+    if (ntile > ninner) {
+      auto k = modwt_inv_pipe_edge<L, kPipeNT, kPipeT, J1, kFMA>;
+      if ((err = prep(k, lds))) return true;
+      hipLaunchKernelGGL(k, dim3((unsigned)(ntile - ninner)), dim3(kPipeNT), lds, s, a.src, a.coef,
+                         a.ldw, a.vout, a.N, ninner, tp);
+      err = hipGetLastError();
+    }
+    return true;
+  }
+}
 template <int L, int J1>
 hipError_t fwd_k(const Bank& b, const ModwtArgs& a, hipStream_t s) {
-  if constexpr (J1 == 8) {
-    switch (geo_f()) {
-      case 1: return fwd_kp<L, J1, true, 512, 8192>(b, a, s);
-      case 3: return fwd_kp<L, J1, true, 256, 4096>(b, a, s);
-      case 4: return fwd_kp<L, J1, true, 512, 4096>(b, a, s);
-      case 5: return fwd_kp<L, J1, true, 1024, 16384>(b, a, s);
-      default:
-        if (p2_bits() & 1) {
-          if ((pf_env() & 1) && run_f() == 1) return fwd_kpp<L, J1, 1024, 8192>(b, a, s);
-          switch (run_f()) {
-            case 3: return fwd_kp<L, J1, true, 1024, 8192, 3>(b, a, s);
-            case 303: return fwd_kp<L, J1, true, 1024, 8192, 303>(b, a, s);
-            case 503: return fwd_kp<L, J1, true, 1024, 8192, 503>(b, a, s);
-            default: break;
-          }
-          return fwd_kp<L, J1, true, 1024, 8192>(b, a, s);
-        }
-        break;
-    }
-  }
-  return (p2_bits() & 1) ? fwd_kp<L, J1, true>(b, a, s) : fwd_kp<L, J1, false>(b, a, s);
+  hipError_t e = hipSuccess;
+  if (fwd_pipe<L, J1>(b, a, s, e)) return e;
+  if constexpr (J1 == 8) return fwd_kp<L, J1, 1024, 8192>(b, a, s);
+  return fwd_kp<L, J1, kNT, kTF>(b, a, s);
 }
 template <int L, int J1>
 hipError_t inv_k(const Bank& b, const ModwtArgs& a, hipStream_t s) {
-  if constexpr (J1 == 8) {
-    switch (geo_i()) {
-      case 1: return inv_kp<L, J1, true, 512, 1024>(b, a, s);
-      case 2: return inv_kp<L, J1, true, 256, 1024>(b, a, s);
-      case 3: return inv_kp<L, J1, true, 1024, 4096>(b, a, s);
-      case 4: return inv_kp<L, J1, true, 256, 2048>(b, a, s);
-      case 5: return inv_kp<L, J1, true, 1024, 4096, 303>(b, a, s);
-      case 6: return inv_kp<L, J1, true, 512, 1536, 303>(b, a, s);
-      case 7: return inv_kp<L, J1, true, 256, 1024, 303>(b, a, s);
-      default:
-        if (p2_bits() & 2) {
-          if (pf_env() & 2) {
-            if (run_m() == 303) return inv_kpp<L, J1, kNT, kTI, 303>(b, a, s);
-            if (run_m() == 1303) return inv_kpp<L, J1, kNT, kTI, 1303>(b, a, s);
-            if (run_m() == 1) return inv_kpp<L, J1, kNT, kTI>(b, a, s);
-          }
-          switch (run_m()) {
-            case 3: return inv_kp<L, J1, true, kNT, kTI, 3>(b, a, s);
-            case 303: return inv_kp<L, J1, true, kNT, kTI, 303>(b, a, s);
-            case 1303: return inv_kp<L, J1, true, kNT, kTI, 1303>(b, a, s);
-            case 503: return inv_kp<L, J1, true, kNT, kTI, 503>(b, a, s);
-            default: break;
-          }
-        }
-        break;
-    }
-  }
-  return (p2_bits() & 2) ? inv_kp<L, J1, true>(b, a, s) : inv_kp<L, J1, false>(b, a, s);
+  hipError_t e = hipSuccess;
+  if (inv_pipe<L, J1>(b, a, s, e)) return e;
+  if constexpr (J1 == 8) return inv_kp<L, J1, 303>(b, a, s);
+  return inv_kp<L, J1, 1>(b, a, s);
 }
 template <int L, bool FWD>
 hipError_t go(const Bank& b, const ModwtArgs& a, hipStream_t s) {

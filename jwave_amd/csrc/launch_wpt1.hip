@@ -37,24 +37,6 @@ hipError_t wfwd1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a.src, a.sv, a.dst, a.dv, a.h, tp);
   return hipGetLastError();
 }
-// env JWV_WPT_ILV (default 1): the reverse tiles' couples as four interleaved
-// sums (rev_couple_ilv); 0 = two rev_pair calls
-bool wpt_ilv() {
-  static const bool v = [] {
-    const char* e = std::getenv("JWV_WPT_ILV");
-    return e ? std::atoi(e) != 0 : true;
-  }();
-  return v;
-}
-// env JWV_WPT_NODMA=1 (diagnostic): the config-4 reverse tile loads its
-// windows through registers instead of LDS-DMA
-bool wpt_nodma() {
-  static const bool v = [] {
-    const char* e = std::getenv("JWV_WPT_NODMA");
-    return e && std::atoi(e) != 0;
-  }();
-  return v;
-}
 // env JWV_WPT_PAD=1: the config-4 reverse tile with padded window strides
 // (conflict-free reads across window boundaries by the bank model)
 bool wpt_pad() {
@@ -64,46 +46,15 @@ bool wpt_pad() {
   }();
   return v;
 }
-// env JWV_WPT_DIAGW=1 (diagnostic only, WRONG results): the config-4 reverse
-// tile's LDS write-back at a 16-B lane stride (its LDS-conflict share)
-bool wpt_diagw() {
-  static const bool v = [] {
-    const char* e = std::getenv("JWV_WPT_DIAGW");
-    return e && std::atoi(e) != 0;
-  }();
-  return v;
-}
-template <int L, int K, bool ILV = false, bool DMA = true>
+// The reverse tiles' couples as four interleaved sums (rev_couple_ilv) for
+// L >= 8: config 4 reverse 2728-2752 -> 2702-2708 us.
+template <int L, int K>
 hipError_t wrev1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
-  if constexpr (!ILV && L >= 8) {
-    if (wpt_ilv()) return wrev1_k<L, K, true>(b, a, s);
-  }
-  if constexpr (ILV && DMA && L == 16 && K == 6) {
-    if (wpt_nodma()) return wrev1_k<L, K, true, false>(b, a, s);
-    if (wpt_pad()) {  // padded window strides (Wpt1RevGeo::stride)
-      auto k = wpt_rev_tile1<L, 256, kWptT, K, kFMA, true, true, 0, true>;
-      const size_t lds = (size_t)Wpt1RevGeo<L, kWptT, K>::lds_doubles(true) * sizeof(double);
-      if (hipError_t e = prep1(k, lds)) return e;
-      RevTaps<L> tp;
-      for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
-      hipLaunchKernelGGL(k, dim3((unsigned)(a.nouter * (a.h / kWptT))), dim3(256), lds, s, a.src,
-                         a.sv, a.dst, a.dv, a.h, tp);
-      return hipGetLastError();
-    }
-    if (wpt_diagw()) {  // diagnostic: conflict-free write-back, wrong results
-      auto k = wpt_rev_tile1<L, 256, kWptT, K, kFMA, true, true, 1>;
-      const size_t lds = (size_t)Wpt1RevGeo<L, kWptT, K>::lds_doubles() * sizeof(double);
-      if (hipError_t e = prep1(k, lds)) return e;
-      RevTaps<L> tp;
-      for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
-      const int hK = a.h;
-      hipLaunchKernelGGL(k, dim3((unsigned)(a.nouter * (a.h / kWptT))), dim3(256), lds, s, a.src,
-                         a.sv, a.dst, a.dv, hK, tp);
-      return hipGetLastError();
-    }
-  }
-  auto k = wpt_rev_tile1<L, 256, kWptT, K, kFMA, ILV, DMA>;
-  const size_t lds = (size_t)Wpt1RevGeo<L, kWptT, K>::lds_doubles() * sizeof(double);
+  constexpr bool ILV = L >= 8;
+  const bool pad = ILV && L == 16 && K == 6 && wpt_pad();
+  auto k = pad ? wpt_rev_tile1<L, 256, kWptT, K, kFMA, ILV, true>
+               : wpt_rev_tile1<L, 256, kWptT, K, kFMA, ILV, false>;
+  const size_t lds = (size_t)Wpt1RevGeo<L, kWptT, K>::lds_doubles(pad) * sizeof(double);
   if (hipError_t e = prep1(k, lds)) return e;
   RevTaps<L> tp;
   for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
@@ -114,71 +65,22 @@ hipError_t wrev1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
 // 8192-sample forward WPT tiles, 512 threads: half the halo recompute of the
 // 4096 tile (14.7% -> 7.4% extra pairs) at the same waves per CU.  Config 4
 // forward 2597 -> 2468 us; the reverse (halo ~7% at 4096) measured no gain
-// and keeps 4096.  env JWV_WPT8K=0: 4096 for both.
-// env JWV_WPT_ILVF (default 0): the same interleaving in the 8192 forward
-// tiles (fwd_couple_ilv).  r03, one box, two rounds: forward 2498 / 2471 us
-// interleaved vs 2488 / 2454 (no gain; the reverse gains 2728 / 2752 -> 2702
-// / 2708 with JWV_WPT_ILV)
-bool wpt_ilvf() {
-  static const bool v = [] {
-    const char* e = std::getenv("JWV_WPT_ILVF");
-    return e ? std::atoi(e) != 0 : false;
-  }();
-  return v;
-}
-// env JWV_WPT_TRI (default 0): the 8192 forward tiles (L = 16) in the triple
-// form (Wpt1FwdLevel3: odd 48-B lane stride, conflict-free reads)
-bool wpt_tri() {
-  static const bool v = [] {
-    const char* e = std::getenv("JWV_WPT_TRI");
-    return e && std::atoi(e) != 0;
-  }();
-  return v;
-}
-template <int L, bool FWD, bool ILV = false>
-hipError_t wpt8k(const Bank& b, const TileArgs& a, hipStream_t s) {
+// and keeps 4096.
+template <int L>
+hipError_t wpt8k_fwd(const Bank& b, const TileArgs& a, hipStream_t s) {
   constexpr int TT = 8192, K = 6;
   const dim3 grid((unsigned)(a.nouter * (a.h / TT)));
-  if constexpr (FWD) {
-    if constexpr (!ILV && L == 16) {
-      if (wpt_tri()) {  // triple form (wpt_fwd_tile1t)
-        auto k = wpt_fwd_tile1t<L, 512, TT, K, kFMA>;
-        const size_t lds = (size_t)Wpt1FwdGeo<L, TT, K>::lds_doubles() * sizeof(double);
-        if (hipError_t e = prep1(k, lds)) return e;
-        FwdTaps<L> tp;
-        for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
-        hipLaunchKernelGGL(k, grid, dim3(512), lds, s, a.src, a.sv, a.dst, a.dv, a.h, tp);
-        return hipGetLastError();
-      }
-    }
-    if constexpr (!ILV && L >= 8)
-      if (wpt_ilvf()) return wpt8k<L, true, true>(b, a, s);
-    auto k = wpt_fwd_tile1<L, 512, TT, K, kFMA, ILV>;
-    const size_t lds = (size_t)Wpt1FwdGeo<L, TT, K>::lds_doubles() * sizeof(double);
-    if (hipError_t e = prep1(k, lds)) return e;
-    FwdTaps<L> tp;
-    for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
-    hipLaunchKernelGGL(k, grid, dim3(512), lds, s, a.src, a.sv, a.dst, a.dv, a.h, tp);
-  } else {
-    auto k = wpt_rev_tile1<L, 512, TT, K, kFMA>;
-    const size_t lds = (size_t)Wpt1RevGeo<L, TT, K>::lds_doubles() * sizeof(double);
-    if (hipError_t e = prep1(k, lds)) return e;
-    RevTaps<L> tp;
-    for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
-    hipLaunchKernelGGL(k, grid, dim3(512), lds, s, a.src, a.sv, a.dst, a.dv, a.h, tp);
-  }
+  auto k = wpt_fwd_tile1<L, 512, TT, K, kFMA>;
+  const size_t lds = (size_t)Wpt1FwdGeo<L, TT, K>::lds_doubles() * sizeof(double);
+  if (hipError_t e = prep1(k, lds)) return e;
+  FwdTaps<L> tp;
+  for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
+  hipLaunchKernelGGL(k, grid, dim3(512), lds, s, a.src, a.sv, a.dst, a.dv, a.h, tp);
   return hipGetLastError();
-}
-bool wpt_8k() {
-  static const bool v = [] {
-    const char* e = std::getenv("JWV_WPT8K");
-    return e ? std::atoi(e) != 0 : true;
-  }();
-  return v;
 }
 template <int L>
 hipError_t wpt1_l(const Bank& b, const TileArgs& a, hipStream_t s, bool fwd) {
-  if (fwd && a.K == 6 && a.h % 8192 == 0 && wpt_8k()) return wpt8k<L, true>(b, a, s);
+  if (fwd && a.K == 6 && a.h % 8192 == 0) return wpt8k_fwd<L>(b, a, s);
   switch (a.K) {
     case 1: return fwd ? wfwd1_k<L, 1>(b, a, s) : wrev1_k<L, 1>(b, a, s);
     case 2: return fwd ? wfwd1_k<L, 2>(b, a, s) : wrev1_k<L, 2>(b, a, s);

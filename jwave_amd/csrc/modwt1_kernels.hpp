@@ -116,7 +116,6 @@ struct ModFwd1Level {
   static constexpr int kPad = ModFwd1Geo<L, T, J0, J1>::kPad;
   // M = m + 100*jr: run form with m pairs per lane on levels j >= jr
   static constexpr int kM = M % 100, kJR = (M / 100) % 10;
-  static constexpr bool kILV = M >= 1000;  // all 4*kM sums interleaved per tap
   static constexpr bool kRun = kM > 1 && j >= kJR;
   __device__ __forceinline__ static void run_p2(const ModwtTaps<L>& tp, double* lds,
                                                 double* __restrict__ wout, int64_t ldw,
@@ -201,170 +200,11 @@ struct ModFwd1Level {
     if constexpr (j < J1)
       ModFwd1Level<L, NT, T, J0, J1, FMA, j + 1, P2, M>::run(tp, lds, wout, ldw, t0, N);
   }
-  // Run form (ModRun): output pair slot s = s0 + m*h, m < M (slot s = window
-  // outputs e0 + 2s, e0 + 2s + 1), reads tap slots s0 + (k - (L-1))*h,
-  // k < M + L - 1 (st = 1: window doubles e0 + 2*s0 - L .. e0 + 2*s0 + 2M - 1).
-  __device__ __forceinline__ static void run_mr(const ModwtTaps<L>& tp, double* lds,
-                                                double* __restrict__ wout, int64_t ldw,
-                                                int64_t t0, int64_t N) {
-    using G = ModFwd1Geo<L, T, J0, J1>;
-    constexpr int st = 1 << (j - 1);
-    constexpr int H = ModRun<L, kM>::template h<st>();
-    constexpr int NRD = ModRun<L, kM>::template nrd<st>();
-    constexpr int e0 = G::e0(j), nout = G::nout(j);
-    static_assert(((kPad + e0) & 1) == 0 && (nout & 1) == 0, "pairs must tile the outputs");
-    constexpr int NS = nout / 2;
-    constexpr int NB = (NS + kM * H - 1) / (kM * H);
-    constexpr int NTASK = NB * H;
-    constexpr int R = (NTASK + NT - 1) / NT;
-    static_assert(G::run_reach(j, kM) <= G::lds_doubles(M), "run reads past the window");
-    const int tid = opaque_tid();
-    double* __restrict__ wrow = wout + (int64_t)(j - 1) * ldw + (t0 - G::S);
-    const bool w16 = (((uintptr_t)wrow + 8 * e0) & 15) == 0;
-    const bool wfast = w16 && t0 + T <= N;  // buffer stores (see run_p2)
-    double* const B = lds + kPad + e0;  // slot 0 of this level, 16-B aligned
-    double2 vv[R][kM];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int t = tid + r * NT;
-      const bool full = (r + 1) * NT <= NTASK;
-      // a wave whose tasks all lie past NTASK skips the slot (scalar branch)
-      if (!full && __builtin_amdgcn_readfirstlane((tid & ~63) + r * NT) >= NTASK) continue;
-      const int tc = full ? t : (t < NTASK ? t : NTASK - 1);
-      const int s0 = ModRun<L, kM>::template slot0<st>(tc);
-      double v[2 * NRD];
-      const double* rb = st == 1 ? B + 2 * s0 - L : B + 2 * s0 - 2 * (L - 1) * H;
-#pragma unroll
-      for (int k = 0; k < NRD; ++k) {
-        const double2 u = *reinterpret_cast<const double2*>(rb + 2 * k * H);
-        v[2 * k] = u.x;
-        v[2 * k + 1] = u.y;
-      }
-      double sw[kM][2], sv[kM][2];
-      if constexpr (kILV) {
-#pragma unroll
-        for (int m = 0; m < kM; ++m) sw[m][0] = sw[m][1] = sv[m][0] = sv[m][1] = 0.0;
-#pragma unroll
-        for (int l = 0; l < L; ++l) {
-#pragma unroll
-          for (int m = 0; m < kM; ++m)
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-              const double x = st == 1 ? v[2 * m + q - l + L] : v[2 * (m - l + L - 1) + q];
-              sw[m][q] = mac<FMA>(sw[m][q], x, tp.h[l]);
-              sv[m][q] = mac<FMA>(sv[m][q], x, tp.g[l]);
-            }
-#pragma unroll
-          for (int m = 0; m < kM; ++m) {
-            pin2(sw[m][0], sw[m][1]);
-            pin2(sv[m][0], sv[m][1]);
-          }
-        }
-      } else {
-#pragma unroll
-        for (int m = 0; m < kM; ++m) {
-#pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            double a = 0.0, c = 0.0;
-#pragma unroll
-            for (int l = 0; l < L; ++l) {
-              const double x = st == 1 ? v[2 * m + q - l + L] : v[2 * (m - l + L - 1) + q];
-              a = mac<FMA>(a, x, tp.h[l]);
-              c = mac<FMA>(c, x, tp.g[l]);
-            }
-            pin2(a, c);
-            sw[m][q] = a;
-            sv[m][q] = c;
-          }
-        }
-      }
-#pragma unroll
-      for (int m = 0; m < kM; ++m) {
-        vv[r][m] = make_double2(sv[m][0], sv[m][1]);
-        const int s = s0 + m * H;
-        const int ee = e0 + 2 * s;  // S has e0's parity: a pair is all halo or all own
-        if ((full || t < NTASK) && s < NS && ee >= G::S) {
-          const int64_t g = t0 + (ee - G::S);
-          if (wfast) {
-            mod_store2(wrow, ee, sw[m][0], sw[m][1]);
-          } else if (w16 && g + 1 < N) {
-            *reinterpret_cast<double2*>(wrow + ee) = make_double2(sw[m][0], sw[m][1]);
-          } else {
-            if (g < N) wrow[ee] = sw[m][0];
-            if (g + 1 < N) wrow[ee + 1] = sw[m][1];
-          }
-        }
-      }
-      asm volatile("" ::: "memory");  // slot fence
-    }
-    lds_barrier();
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int t = tid + r * NT;
-      const bool ok = (r + 1) * NT <= NTASK || t < NTASK;
-      const int s0 = ModRun<L, kM>::template slot0<st>(ok ? t : 0);
-#pragma unroll
-      for (int m = 0; m < kM; ++m) {
-        const int s = s0 + m * H;
-        if (ok && s < NS) *reinterpret_cast<double2*>(B + 2 * s) = vv[r][m];
-      }
-    }
-    lds_barrier();
-    if constexpr (j < J1)
-      ModFwd1Level<L, NT, T, J0, J1, FMA, j + 1, P2, M>::run(tp, lds, wout, ldw, t0, N);
-  }
   __device__ __forceinline__ static void run(const ModwtTaps<L>& tp, double* lds,
                                              double* __restrict__ wout, int64_t ldw, int64_t t0,
                                              int64_t N) {
-    if constexpr (kRun) {
-      run_mr(tp, lds, wout, ldw, t0, N);
-      return;
-    } else if constexpr (P2) {
-      run_p2(tp, lds, wout, ldw, t0, N);
-      return;
-    }
-    using G = ModFwd1Geo<L, T, J0, J1>;
-    constexpr int st = 1 << (j - 1);
-    constexpr int e0 = G::e0(j), nout = G::nout(j);
-    constexpr int R = (nout + NT - 1) / NT;
-    const int tid = opaque_tid();
-    // W_j[g] for window index e: g = t0 + e - S (stored only for e >= S)
-    double* __restrict__ wrow = wout + (int64_t)(j - 1) * ldw + (t0 - G::S);
-    double vv[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int p = tid + r * NT;
-      const bool full = (r + 1) * NT <= nout;  // compile-time per slot
-      const bool v = full || p < nout;
-      const int pc = full ? p : (v ? p : nout - 1);
-      const double* b = lds + e0 + pc;
-      double x[L];
-#pragma unroll
-      for (int l = 0; l < L; ++l) x[l] = b[-l * st];
-      double sw = 0.0, sv = 0.0;
-#pragma unroll
-      for (int l = 0; l < L; ++l) {
-        sw = mac<FMA>(sw, x[l], tp.h[l]);
-        sv = mac<FMA>(sv, x[l], tp.g[l]);
-      }
-      pin2(sw, sv);
-      vv[r] = sv;
-      const int e = e0 + p;
-      // outputs of the tile's own range: e >= S, inside the signal
-      if (v && (e0 + (r + 1) * NT - 1 < G::S ? false : e >= G::S) && t0 + (e - G::S) < N)
-        wrow[e] = sw;
-      if constexpr (JWV_MOD1_FENCE > 0)
-        if ((r + 1) % JWV_MOD1_FENCE == 0) asm volatile("" : "+v"(vv[r]) :: "memory");
-    }
-    lds_barrier();
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int p = tid + r * NT;
-      if ((r + 1) * NT <= nout || p < nout) lds[e0 + p] = vv[r];
-    }
-    lds_barrier();
-    if constexpr (j < J1)
-      ModFwd1Level<L, NT, T, J0, J1, FMA, j + 1, P2, M>::run(tp, lds, wout, ldw, t0, N);
+    static_assert(P2 && M == 1, "forward: the P2 form");
+    run_p2(tp, lds, wout, ldw, t0, N);
   }
 };
 
@@ -393,63 +233,6 @@ __global__ __launch_bounds__(NT) void modwt_fwd_tile1(const double* __restrict__
   for (int r = 0; r < (T + NT - 1) / NT; ++r) {
     const int p = tid + r * NT;
     if (p < T && t0 + p < N) vout[t0 + p] = lds[pad + G::S + p];
-  }
-}
-
-// Persistent form of modwt_fwd_tile1: one block per CU walks the tiles of its
-// XCD's contiguous chunk (the chunk's blocks side by side, so a tile's halo is
-// a sibling's samples in the same L2) and loads the NEXT tile's window into
-// registers (buffer loads, in flight through all of this tile's levels) right
-// after this tile's window is in LDS: at one 80-KB block per CU the window load
-// is otherwise exposed at every tile start.  Same levels, same outputs.
-// Grid: 8 * blocks per XCD.
-template <int L, int NT, int T, int J0, int J1, bool FMA, bool P2 = false, int M = 1>
-__global__ __launch_bounds__(NT) void modwt_fwd_tile1p(const double* __restrict__ src,
-                                                       double* __restrict__ wout, int64_t ldw,
-                                                       double* __restrict__ vout, int64_t N,
-                                                       ModwtTaps<L> tp) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  using G = ModFwd1Geo<L, T, J0, J1>;
-  constexpr int MAXP = (G::W + NT - 1) / NT;
-  constexpr int pad = (P2 || M % 100 > 1) ? G::kPad : 0;
-  const int tid = threadIdx.x;
-  const int64_t ntile = (N + T - 1) / T;
-  const int x = blockIdx.x & 7, nbx = gridDim.x >> 3, bx = blockIdx.x >> 3;
-  const int64_t q = ntile >> 3, rr = ntile & 7;
-  const int64_t c0 = x * q + (x < rr ? x : rr), c1 = c0 + q + (x < rr ? 1 : 0);
-  auto inside_at = [&](int64_t t0) { return t0 - G::S >= 0 && t0 + T <= N; };
-  double pv[MAXP];
-  bool have = false;
-  for (int64_t tile = c0 + bx; tile < c1; tile += nbx) {
-    const int64_t t0 = tile * T;
-    if (have) {
-#pragma unroll
-      for (int r = 0; r < MAXP; ++r)
-        if ((r + 1) * NT <= G::W || tid + r * NT < G::W) lds[pad + tid + r * NT] = pv[r];
-    } else if (inside_at(t0)) {
-      mod_load_window<NT, MAXP>(lds + pad, src + (t0 - G::S), G::W);
-    } else {
-      load_window<1, NT, MAXP>(lds + pad, src, G::W, false, 0, 1,
-                               [&](int e) { return wrap_mod(t0 - G::S + e, N); });
-    }
-    lds_barrier();
-    const int64_t tn = tile + nbx;
-    have = tn < c1 && inside_at(tn * T);
-    if (have) {
-      const auto rs = mod_rsrc(src + (tn * T - G::S));
-#pragma unroll
-      for (int r = 0; r < MAXP; ++r)
-        if ((r + 1) * NT <= G::W || tid + r * NT < G::W)
-          pv[r] = __builtin_bit_cast(
-              double, __builtin_amdgcn_raw_buffer_load_b64(rs, tid * 8, r * NT * 8, 0));
-    }
-    ModFwd1Level<L, NT, T, J0, J1, FMA, J0, P2, M>::run(tp, lds, wout, ldw, t0, N);
-#pragma unroll
-    for (int r = 0; r < (T + NT - 1) / NT; ++r) {
-      const int p = tid + r * NT;
-      if (p < T && t0 + p < N) vout[t0 + p] = lds[pad + G::S + p];
-    }
-    lds_barrier();  // LDS reuse by the next tile
   }
 }
 
@@ -491,9 +274,8 @@ struct ModInv1Geo {
 template <int L, int NT, int T, int J0, int J1, bool FMA, int j, bool P2 = false, int M = 1>
 struct ModInv1Level {
   using G = ModInv1Geo<L, T, J0, J1>;
-  // M = m + 100*jr (+ 1000: tap-major interleaved run sums, run_sums_ilv)
+  // M = m + 100*jr: run form with m pairs per lane on levels j >= jr
   static constexpr int kM = M % 100, kJR = (M / 100) % 10;
-  static constexpr bool kILV = M >= 1000;
   static constexpr bool kRun = kM > 1 && j >= kJR;
   static constexpr int MAXP = (G::Wmax + NT - 1) / NT;
   // fetch the W_j window [t0, t0 + T + Rin(j)) into registers
@@ -525,11 +307,9 @@ struct ModInv1Level {
   __device__ __forceinline__ static void run(const ModwtTaps<L>& tp, double* vb, double* wb,
                                              double (&pw)[MAXP], const double* __restrict__ coef,
                                              int64_t ldw, double* __restrict__ dst, int64_t t0,
-                                             int64_t N, bool inside, int64_t tn = -1,
-      bool inn = false) {
-    constexpr int st = 1 << (j - 1);
-    constexpr int Wn = T + G::Rin(j), nout = T + G::Rout(j);
-    constexpr int R = (nout + NT - 1) / NT;
+                                             int64_t N, bool inside) {
+    static_assert(P2, "inverse: the P2 or run form");
+    constexpr int Wn = T + G::Rin(j);
     const int tid = opaque_tid();
 #pragma unroll
     for (int r = 0; r < MAXP; ++r) {
@@ -539,57 +319,10 @@ struct ModInv1Level {
     lds_barrier();
     if constexpr (j > J0)
       ModInv1Level<L, NT, T, J0, J1, FMA, j - 1, P2, M>::fetch(pw, coef, ldw, t0, N, inside);
-    else if (tn >= 0)  // persistent form: the next tile's top W window
-      ModInv1Level<L, NT, T, J0, J1, FMA, J1, P2, M>::fetch(pw, coef, ldw, tn, N, inn);
-    if constexpr (kRun) {
-      compute_mr(tp, vb, wb, pw, coef, ldw, dst, t0, N, inside, tn, inn);
-      return;
-    } else if constexpr (P2) {
-      compute_p2(tp, vb, wb, pw, coef, ldw, dst, t0, N, inside, tn, inn);
-      return;
-    }
-    double vv[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int p = tid + r * NT;
-      const bool full = (r + 1) * NT <= nout;
-      const int pc = full ? p : (p < nout ? p : nout - 1);
-      const double* a = vb + pc;
-      const double* w = wb + pc;
-      double xv[L], xw[L];
-#pragma unroll
-      for (int l = 0; l < L; ++l) {
-        xv[l] = a[l * st];
-        xw[l] = w[l * st];
-      }
-      double sa = 0.0, sd = 0.0;
-#pragma unroll
-      for (int l = 0; l < L; ++l) {
-        sa = mac<FMA>(sa, xv[l], tp.g[l]);
-        sd = mac<FMA>(sd, xw[l], tp.h[l]);
-      }
-      pin2(sa, sd);
-      vv[r] = sa + sd;
-      if constexpr (JWV_MOD1_FENCE > 0)
-        if ((r + 1) % JWV_MOD1_FENCE == 0) asm volatile("" : "+v"(vv[r]) :: "memory");
-    }
-    lds_barrier();
-    if constexpr (j == J0) {
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int p = tid + r * NT;
-        if (r * NT < T && (p < T) && t0 + p < N) dst[t0 + p] = vv[r];
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int p = tid + r * NT;
-        if ((r + 1) * NT <= nout || p < nout) vb[p] = vv[r];
-      }
-      // (the barrier after the next level's W write orders these)
-      ModInv1Level<L, NT, T, J0, J1, FMA, j - 1, P2, M>::run(tp, vb, wb, pw, coef, ldw, dst, t0, N,
-                                                          inside, tn, inn);
-    }
+    if constexpr (kRun)
+      compute_mr(tp, vb, wb, pw, coef, ldw, dst, t0, N, inside);
+    else
+      compute_p2(tp, vb, wb, pw, coef, ldw, dst, t0, N, inside);
   }
   // P2: a lane computes the adjacent outputs (p, p+1), p even: every tap pair
   // (p + l*st, p + 1 + l*st) of V and of W is one 16-B LDS read (st = 1: the
@@ -599,8 +332,7 @@ struct ModInv1Level {
                                                     double (&pw)[MAXP],
                                                     const double* __restrict__ coef, int64_t ldw,
                                                     double* __restrict__ dst, int64_t t0,
-                                                    int64_t N, bool inside, int64_t tn = -1,
-      bool inn = false) {
+                                                    int64_t N, bool inside) {
     constexpr int st = 1 << (j - 1);
     constexpr int nout = T + G::Rout(j);
     constexpr int NP = (nout + 1) / 2;
@@ -683,7 +415,7 @@ struct ModInv1Level {
         if ((r + 1) * NT <= NP || k < NP) *reinterpret_cast<double2*>(vb + 2 * k) = vv[r];
       }
       ModInv1Level<L, NT, T, J0, J1, FMA, j - 1, P2, M>::run(tp, vb, wb, pw, coef, ldw, dst, t0, N,
-                                                          inside, tn, inn);
+                                                          inside);
     }
   }
   // Run form (ModRun): output pair slot s = s0 + m*h, m < M, reads tap slots
@@ -718,44 +450,11 @@ struct ModInv1Level {
       }
     }
   }
-  // run_sums with the tap loop outermost and every accumulator materialised
-  // after each tap: the 2*M independent chains stay interleaved (the compiler
-  // otherwise schedules them one after the other, each add waiting on the
-  // previous one).  Same per-output summation order.
-  template <bool ISW>
-  __device__ __forceinline__ static void run_sums_ilv(const ModwtTaps<L>& tp, const double* base,
-                                                      double (&acc)[kM][2]) {
-    constexpr int st = 1 << (j - 1);
-    constexpr int H = ModRun<L, kM>::template h<st>();
-    constexpr int NRD = ModRun<L, kM>::template nrd<st>();
-    double v[2 * NRD];
-#pragma unroll
-    for (int k = 0; k < NRD; ++k) {
-      const double2 u = *reinterpret_cast<const double2*>(base + 2 * k * H);
-      v[2 * k] = u.x;
-      v[2 * k + 1] = u.y;
-    }
-#pragma unroll
-    for (int m = 0; m < kM; ++m) acc[m][0] = acc[m][1] = 0.0;
-#pragma unroll
-    for (int l = 0; l < L; ++l) {
-#pragma unroll
-      for (int m = 0; m < kM; ++m)
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const double x = st == 1 ? v[2 * m + q + l] : v[2 * (m + l) + q];
-          acc[m][q] = mac<FMA>(acc[m][q], x, ISW ? tp.h[l] : tp.g[l]);
-        }
-#pragma unroll
-      for (int m = 0; m < kM; ++m) pin2(acc[m][0], acc[m][1]);
-    }
-  }
   __device__ __forceinline__ static void compute_mr(const ModwtTaps<L>& tp, double* vb, double* wb,
                                                     double (&pw)[MAXP],
                                                     const double* __restrict__ coef, int64_t ldw,
                                                     double* __restrict__ dst, int64_t t0,
-                                                    int64_t N, bool inside, int64_t tn = -1,
-      bool inn = false) {
+                                                    int64_t N, bool inside) {
     constexpr int st = 1 << (j - 1);
     constexpr int H = ModRun<L, kM>::template h<st>();
     constexpr int nout = G::nout(j);
@@ -775,13 +474,8 @@ struct ModInv1Level {
       const int tc = full ? t : (t < NTASK ? t : NTASK - 1);
       const int s0 = ModRun<L, kM>::template slot0<st>(tc);
       double sa[kM][2], sd[kM][2];
-      if constexpr (kILV) {
-        run_sums_ilv<false>(tp, vb + 2 * s0, sa);
-        run_sums_ilv<true>(tp, wb + 2 * s0, sd);
-      } else {
-        run_sums<false>(tp, vb + 2 * s0, sa);
-        run_sums<true>(tp, wb + 2 * s0, sd);
-      }
+      run_sums<false>(tp, vb + 2 * s0, sa);
+      run_sums<true>(tp, wb + 2 * s0, sd);
 #pragma unroll
       for (int m = 0; m < kM; ++m) {
         pin2(sa[m][0], sd[m][0]);
@@ -819,7 +513,7 @@ struct ModInv1Level {
     }
     if constexpr (j > J0)
       ModInv1Level<L, NT, T, J0, J1, FMA, j - 1, P2, M>::run(tp, vb, wb, pw, coef, ldw, dst, t0, N,
-                                                          inside, tn, inn);
+                                                          inside);
   }
 };
 
@@ -844,60 +538,6 @@ __global__ __launch_bounds__(NT) void modwt_inv_tile1(const double* __restrict__
                                   [&](int e) { return wrap_mod(t0 + e, N); });
   Top::fetch(pw, coef, ldw, t0, N, inside);
   Top::run(tp, vb, wb, pw, coef, ldw, dst, t0, N, inside);
-}
-
-// Persistent form of modwt_inv_tile1 (as modwt_fwd_tile1p): blocks walk their
-// XCD's chunk of tiles; the next tile's V window is loaded into registers at
-// this tile's start and its top W window in this tile's last level, so both
-// are in flight while this tile computes.  Same levels, same outputs.
-template <int L, int NT, int T, int J0, int J1, bool FMA, bool P2 = false, int M = 1>
-__global__ __launch_bounds__(NT) void modwt_inv_tile1p(const double* __restrict__ vsrc,
-                                                       const double* __restrict__ coef, int64_t ldw,
-                                                       double* __restrict__ dst, int64_t N,
-                                                       ModwtTaps<L> tp) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  using G = ModInv1Geo<L, T, J0, J1>;
-  using Top = ModInv1Level<L, NT, T, J0, J1, FMA, J1, P2, M>;
-  constexpr int MAXP = Top::MAXP;
-  double* vb = lds;
-  double* wb = lds + (M % 100 > 1 ? G::run_buf(M) : G::buf());
-  const int tid = threadIdx.x;
-  const int64_t ntile = (N + T - 1) / T;
-  const int x = blockIdx.x & 7, nbx = gridDim.x >> 3, bx = blockIdx.x >> 3;
-  const int64_t q = ntile >> 3, rr = ntile & 7;
-  const int64_t c0 = x * q + (x < rr ? x : rr), c1 = c0 + q + (x < rr ? 1 : 0);
-  double pw[MAXP], pv[MAXP];
-  bool have = false;  // pv holds this tile's V window, pw its top W window
-  for (int64_t tile = c0 + bx; tile < c1; tile += nbx) {
-    const int64_t t0 = tile * T;
-    const bool inside = t0 + G::Wmax <= N;
-    if (have) {
-#pragma unroll
-      for (int r = 0; r < MAXP; ++r)
-        if ((r + 1) * NT <= G::Wmax || tid + r * NT < G::Wmax) vb[tid + r * NT] = pv[r];
-    } else {
-      if (inside)
-        mod_load_window<NT, MAXP>(vb, vsrc + t0, G::Wmax);
-      else
-        load_window<1, NT, MAXP>(vb, vsrc, G::Wmax, false, 0, 1,
-                                 [&](int e) { return wrap_mod(t0 + e, N); });
-      Top::fetch(pw, coef, ldw, t0, N, inside);
-    }
-    const int64_t tn = tile + nbx < c1 ? (tile + nbx) * T : -1;
-    have = tn >= 0 && tn + G::Wmax <= N;
-    if (have) {
-      const auto rs = mod_rsrc(vsrc + tn);
-#pragma unroll
-      for (int r = 0; r < MAXP; ++r)
-        if ((r + 1) * NT <= G::Wmax || tid + r * NT < G::Wmax)
-          pv[r] = __builtin_bit_cast(
-              double, __builtin_amdgcn_raw_buffer_load_b64(rs, tid * 8, r * NT * 8, 0));
-    }
-    // the last level fetches the next tile's top W window only when it is
-    // prefetched as a whole (have); otherwise the next tile loads both itself
-    Top::run(tp, vb, wb, pw, coef, ldw, dst, t0, N, inside, have ? tn : -1, true);
-    lds_barrier();  // LDS reuse by the next tile
-  }
 }
 
 }  // namespace jwv

@@ -231,264 +231,6 @@ __global__ __launch_bounds__(256) void modwt_inv_level(const double* __restrict_
   }
 }
 
-// Inverse tile with the W windows prefetched two levels ahead (two register
-// buffers): a level's compute is shorter than an HBM round trip under load,
-// so one level of look-ahead left most of the W latency exposed (SQ_WAIT_ANY
-// ~54% of wave cycles in modwt_inv_tile).  Same math and order as
-// modwt_inv_tile.
-template <int L, int NT, int T, int SMAX, bool FMA>
-__global__ __launch_bounds__(NT) void modwt_inv_tile2(const double* __restrict__ vsrc,
-                                                      const double* __restrict__ coef, int64_t ldw,
-                                                      double* __restrict__ dst, int64_t N, int j0,
-                                                      int j1, typename MB<L>::Arg tp) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  constexpr int MAXP = (T + SMAX + NT - 1) / NT;
-  const int nL = MB<L>::n(tp);
-  const int R = (nL - 1) * ((1 << j1) - (1 << (j0 - 1)));
-  double* vb = lds;
-  double* wb = lds + (T + R);
-  const int64_t t0 = xcd_tile() * T;
-  const int tid = threadIdx.x;
-  auto fetch_w = [&](double (&pw)[MAXP], int j, int W) {
-    const double* wrow = coef + (int64_t)(j - 1) * ldw;
-#pragma unroll
-    for (int r = 0; r < MAXP; ++r) {
-      const int q = tid + r * NT;
-      pw[r] = q < W ? wrow[wrap_mod(t0 + q, N)] : 0.0;
-    }
-  };
-  // right halo still needed at the input of level j (Rj(j1) = R)
-  auto halo_at = [&](int j) { return (nL - 1) * ((1 << j) - (1 << (j0 - 1))); };
-  double pa[MAXP], pb[MAXP];
-  load_window<1, NT, MAXP>(vb, vsrc, T + R, false, 0, 1,
-                           [&](int e) { return wrap_mod(t0 + e, N); });
-  fetch_w(pa, j1, T + R);
-  if (j1 - 1 >= j0) fetch_w(pb, j1 - 1, T + halo_at(j1 - 1));
-  auto level = [&](double (&cur)[MAXP], int j) {
-    const int st = 1 << (j - 1);
-    const int Rj = halo_at(j);
-    const int Rn = Rj - (nL - 1) * st;
-#pragma unroll
-    for (int r = 0; r < MAXP; ++r) {
-      const int q = tid + r * NT;
-      if (q < T + Rj) wb[q] = cur[r];
-    }
-    lds_barrier();
-    if (j - 2 >= j0) fetch_w(cur, j - 2, T + halo_at(j - 2));  // two levels ahead
-    const int nout = T + Rn;
-    double vv[MAXP];
-#pragma unroll
-    for (int r = 0; r < MAXP; ++r) {
-      const int p = tid + r * NT;
-      if (p < nout) {
-        double sa = 0.0, sd = 0.0;
-#pragma unroll
-        for (int l = 0; l < MB<L>::n(tp); ++l) {
-          sa = mac<FMA>(sa, vb[p + l * st], tp.g[l]);
-          sd = mac<FMA>(sd, wb[p + l * st], tp.h[l]);
-        }
-        vv[r] = sa + sd;
-      }
-    }
-    lds_barrier();
-    if (j == j0) {
-#pragma unroll
-      for (int r = 0; r < MAXP; ++r) {
-        const int p = tid + r * NT;
-        if (p < T && t0 + p < N) dst[t0 + p] = vv[r];
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < MAXP; ++r) {
-        const int p = tid + r * NT;
-        if (p < nout) vb[p] = vv[r];
-      }
-    }
-  };
-  for (int j = j1; j >= j0; j -= 2) {
-    level(pa, j);
-    if (j - 1 >= j0) level(pb, j - 1);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Register-blocked tiles (compile-time L only).  At level j the taps sit st =
-// 2^(j-1) apart, so outputs p, p+st, ..., p+(KO-1)st share all but KO-1 of
-// their inputs: one lane computes those KO outputs from KO+L-1 window reads
-// instead of KO*L.  LDS read traffic drops ~L*KO/(L+KO-1)-fold (D4, KO=4:
-// 2.9x), which is what bounded the per-level loop of the plain tiles above.
-// Lane work item u -> (group g = u / st, phase r = u % st); its outputs are
-// p_i = g*KO*st + r + i*st.  Each output still sums its taps l = 0..L-1 in
-// ascending order from 0.0, so EXACT results are unchanged bit for bit.
-template <int L, int NT, int T, int SMAX, int KO>
-struct ModGeoG {
-  // work items per level <= ceil(nout/(KO*st))*st <= nout/KO + st; st <= 2^12
-  // at the deepest fused level only when the halo is small, so bound by the
-  // window: (T + SMAX)/KO + (SMAX/(L-1) + 1).
-  static constexpr int kItems = (T + SMAX) / KO + SMAX / (L > 1 ? L - 1 : 1) + 1;
-  static constexpr int kSlots = (kItems + NT - 1) / NT;
-};
-
-template <int L, int NT, int T, int SMAX, int KO, bool FMA>
-__global__ __launch_bounds__(NT) void modwt_fwd_tile_g(const double* __restrict__ src,
-                                                       double* __restrict__ wout, int64_t ldw,
-                                                       double* __restrict__ vout, int64_t N, int j0,
-                                                       int j1, ModwtTaps<L> tp) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  constexpr int MAXP = (T + SMAX + NT - 1) / NT;
-  constexpr int NS = ModGeoG<L, NT, T, SMAX, KO>::kSlots;
-  const int S = (L - 1) * ((1 << j1) - (1 << (j0 - 1)));
-  const int64_t t0 = xcd_tile() * T;
-  const int tid = threadIdx.x;
-  const int W = T + S;
-  load_window<1, NT, MAXP>(lds, src, W, false, 0, 1,
-                           [&](int e) { return wrap_mod(t0 - S + e, N); });
-  lds_barrier();
-  int Sj = S;
-  for (int j = j0; j <= j1; ++j) {
-    const int sh = j - 1, st = 1 << sh;
-    const int Sn = Sj - (L - 1) * st;
-    const int e0 = S - Sn;
-    const int nout = T + Sn;
-    const int span = KO << sh;                       // outputs covered by one group
-    const int nitems = ((nout + span - 1) / span) << sh;
-    double* wrow = wout + (int64_t)(j - 1) * ldw;
-    double vv[NS][KO];
-#pragma unroll
-    for (int sl = 0; sl < NS; ++sl) {
-      const int u = tid + sl * NT;
-      if (u < nitems) {
-        const int pb = (u >> sh) * span + (u & (st - 1));  // p_0
-        const int eb = e0 + pb - (L - 1) * st;              // window index of x[0]
-        double x[KO + L - 1];
-#pragma unroll
-        for (int m = 0; m < KO + L - 1; ++m) {
-          const int e = eb + m * st;
-          x[m] = e < W ? lds[e] : 0.0;
-        }
-#pragma unroll
-        for (int i = 0; i < KO; ++i) {
-          double sw = 0.0, sv = 0.0;
-#pragma unroll
-          for (int l = 0; l < L; ++l) {
-            const double v = x[i - l + (L - 1)];  // lds[e0 + p_i - l*st]
-            sw = mac<FMA>(sw, v, tp.h[l]);
-            sv = mac<FMA>(sv, v, tp.g[l]);
-          }
-          vv[sl][i] = sv;
-          const int p = pb + i * st;
-          const int64_t g = t0 + (e0 + p - S);
-          if (p < nout && e0 + p >= S && g < N) wrow[g] = sw;
-        }
-      }
-    }
-    lds_barrier();
-#pragma unroll
-    for (int sl = 0; sl < NS; ++sl) {
-      const int u = tid + sl * NT;
-      if (u < nitems) {
-        const int pb = (u >> sh) * span + (u & (st - 1));
-#pragma unroll
-        for (int i = 0; i < KO; ++i)
-          if (pb + i * st < nout) lds[e0 + pb + i * st] = vv[sl][i];
-      }
-    }
-    lds_barrier();
-    Sj = Sn;
-  }
-  for (int p = tid; p < T; p += NT) {
-    const int64_t g = t0 + p;
-    if (g < N) vout[g] = lds[S + p];
-  }
-}
-
-template <int L, int NT, int T, int SMAX, int KO, bool FMA>
-__global__ __launch_bounds__(NT) void modwt_inv_tile_g(const double* __restrict__ vsrc,
-                                                       const double* __restrict__ coef, int64_t ldw,
-                                                       double* __restrict__ dst, int64_t N, int j0,
-                                                       int j1, ModwtTaps<L> tp) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  constexpr int MAXP = (T + SMAX + NT - 1) / NT;
-  constexpr int NS = ModGeoG<L, NT, T, SMAX, KO>::kSlots;
-  const int R = (L - 1) * ((1 << j1) - (1 << (j0 - 1)));
-  double* vb = lds;
-  double* wb = lds + (T + R);
-  const int64_t t0 = xcd_tile() * T;
-  const int tid = threadIdx.x;
-  double pw[MAXP];
-  auto fetch_w = [&](int j, int W) {
-    const double* wrow = coef + (int64_t)(j - 1) * ldw;
-#pragma unroll
-    for (int r = 0; r < MAXP; ++r) {
-      const int q = tid + r * NT;
-      pw[r] = q < W ? wrow[wrap_mod(t0 + q, N)] : 0.0;
-    }
-  };
-  load_window<1, NT, MAXP>(vb, vsrc, T + R, false, 0, 1,
-                           [&](int e) { return wrap_mod(t0 + e, N); });
-  fetch_w(j1, T + R);
-  int Rj = R;
-  for (int j = j1; j >= j0; --j) {
-    const int sh = j - 1, st = 1 << sh;
-    const int Rn = Rj - (L - 1) * st;
-    const int Wl = T + Rj;  // this level's window length
-#pragma unroll
-    for (int r = 0; r < MAXP; ++r) {
-      const int q = tid + r * NT;
-      if (q < Wl) wb[q] = pw[r];
-    }
-    lds_barrier();
-    if (j > j0) fetch_w(j - 1, T + Rn);
-    const int nout = T + Rn;
-    const int span = KO << sh;
-    const int nitems = ((nout + span - 1) / span) << sh;
-    double vv[NS][KO];
-#pragma unroll
-    for (int sl = 0; sl < NS; ++sl) {
-      const int u = tid + sl * NT;
-      if (u < nitems) {
-        const int pb = (u >> sh) * span + (u & (st - 1));
-        double xv[KO + L - 1], xw[KO + L - 1];
-#pragma unroll
-        for (int m = 0; m < KO + L - 1; ++m) {
-          const int q = pb + m * st;
-          const bool ok = q < Wl;
-          xv[m] = ok ? vb[q] : 0.0;
-          xw[m] = ok ? wb[q] : 0.0;
-        }
-#pragma unroll
-        for (int i = 0; i < KO; ++i) {
-          double sa = 0.0, sd = 0.0;
-#pragma unroll
-          for (int l = 0; l < L; ++l) {
-            sa = mac<FMA>(sa, xv[i + l], tp.g[l]);
-            sd = mac<FMA>(sd, xw[i + l], tp.h[l]);
-          }
-          vv[sl][i] = sa + sd;
-        }
-      }
-    }
-    lds_barrier();
-#pragma unroll
-    for (int sl = 0; sl < NS; ++sl) {
-      const int u = tid + sl * NT;
-      if (u < nitems) {
-        const int pb = (u >> sh) * span + (u & (st - 1));
-#pragma unroll
-        for (int i = 0; i < KO; ++i) {
-          const int p = pb + i * st;
-          if (j == j0) {
-            if (p < T && t0 + p < N) dst[t0 + p] = vv[sl][i];
-          } else if (p < nout) {
-            vb[p] = vv[sl][i];
-          }
-        }
-      }
-    }
-    Rj = Rn;
-  }
-}
-
 // ---------------------------------------------------------------------------
 // Inverse tile in class-major ("polyphase") LDS layout (compile-time L).
 // At level j the taps of output p sit st = 2^(j-1) apart, so each residue

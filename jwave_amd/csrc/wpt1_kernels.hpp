@@ -28,12 +28,11 @@ namespace jwv {
 template <int L, int T, int K>
 struct Wpt1FwdGeo {
   static constexpr int m(int l) { return (T >> l) + (L - 2) * ((1 << (K - l)) - 1); }
-  // + 6: the triple form reads up to 3 samples past a sub-window
-  static constexpr int lds_doubles() { return m(0) + 6; }
+  static constexpr int lds_doubles() { return m(0) + 2; }
   static_assert((L & 1) == 0 && ((T >> K) & 1) == 0, "even windows");
 };
 
-template <int L, int NT, int T, int K, bool FMA, int l, bool ILV = false>
+template <int L, int NT, int T, int K, bool FMA, int l>
 struct Wpt1FwdLevel {
   // lds: 2^(l-1) input sub-windows of m(l-1) samples (stride m(l-1)).
   __device__ __forceinline__ static void run(const FwdTaps<L>& tp, double* lds, int h, int t,
@@ -60,12 +59,8 @@ struct Wpt1FwdLevel {
           x[j + 1] = v.y;
         }
         double a0, d0, a1, d1;
-        if constexpr (ILV) {
-          fwd_couple_ilv<L, FMA>(tp, x, a0, d0, a1, d1);
-        } else {
-          fwd_pair<L, FMA>(tp, [&](int j) { return x[j]; }, a0, d0);
-          fwd_pair<L, FMA>(tp, [&](int j) { return x[j + 2]; }, a1, d1);
-        }
+        fwd_pair<L, FMA>(tp, [&](int j) { return x[j]; }, a0, d0);
+        fwd_pair<L, FMA>(tp, [&](int j) { return x[j + 2]; }, a1, d1);
         // slot boundary: results exist here and later slots' LDS reads stay
         // below, so the compiler cannot hoist all slots' windows at once
         // (L = 16: ~190 VGPRs, 2 waves/SIMD -> ~80 VGPRs)
@@ -93,14 +88,14 @@ struct Wpt1FwdLevel {
         }
       }
       lds_barrier();
-      Wpt1FwdLevel<L, NT, T, K, FMA, l + 1, ILV>::run(tp, lds, h, t, y);
+      Wpt1FwdLevel<L, NT, T, K, FMA, l + 1>::run(tp, lds, h, t, y);
     }
   }
 };
 
 // Grid: rows * (h / T) blocks; row o = packet o of the pass input (view sv,
 // packets addressed through view_base); output rows likewise (view dv).
-template <int L, int NT, int T, int K, bool FMA, bool ILV = false>
+template <int L, int NT, int T, int K, bool FMA>
 __global__ __launch_bounds__(NT) void wpt_fwd_tile1(const double* __restrict__ src, AxisView sv,
                                                     double* __restrict__ dst, AxisView dv, int h,
                                                     FwdTaps<L> tp) {
@@ -118,107 +113,7 @@ __global__ __launch_bounds__(NT) void wpt_fwd_tile1(const double* __restrict__ s
   load_window<1, NT, (M0 + NT - 1) / NT>(lds, s, M0, true, 0, 1,
                                           [&](int e) { return (int64_t)((base + e) & msk); });
   dma_fence_barrier();
-  Wpt1FwdLevel<L, NT, T, K, FMA, 1, ILV>::run(tp, lds, h, t, dst + view_base(dv, o));
-}
-
-// Triple form of Wpt1FwdLevel: a lane computes three adjacent pairs (i0,
-// i0+1, i0+2) of one sub-window from L+4 window samples read as (L+4)/2
-// 16-B LDS reads.  Lanes sit 48 B (3 slots) apart, an odd slot stride, so a
-// 16-lane ds_read_b128 group covers 16 distinct slots mod 16 (the couples'
-// 32-B stride covers 8: 2-way conflicts on every read), and each pair costs
-// 10/3 reads instead of 9/2.  The write-back (three 8-B stores per operand at
-// a 24-B lane stride) is conflict-free as well.  Same per-output order
-// (fwd_pair), so EXACT results are unchanged.
-template <int L, int NT, int T, int K, bool FMA, int l>
-struct Wpt1FwdLevel3 {
-  __device__ __forceinline__ static void run(const FwdTaps<L>& tp, double* lds, int h, int t,
-                                             double* __restrict__ y) {
-    using G = Wpt1FwdGeo<L, T, K>;
-    constexpr int mi = G::m(l - 1), mo = G::m(l);
-    constexpr int N3 = (mo + 2) / 3;                // triples per sub-window
-    constexpr int NC = (1 << (l - 1)) * N3;         // triples of the level
-    constexpr int R = (NC + NT - 1) / NT;
-    const int tid = opaque_tid();
-    double ra[R][3], rd[R][3];
-    int wo[R];  // write-back offset (2s)*mo + i0
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int q = tid + r * NT;
-      if ((r + 1) * NT <= NC || q < NC) {
-        const int s = q / N3, i0 = 3 * (q % N3);
-        wo[r] = (2 * s) * mo + i0;
-        const double* in = lds + s * mi + 2 * i0;  // 16-B aligned: mi even, 2*i0 = 6u
-        double x[L + 4];
-#pragma unroll
-        for (int j = 0; j < L + 4; j += 2) {
-          const double2 v = *reinterpret_cast<const double2*>(in + j);
-          x[j] = v.x;
-          x[j + 1] = v.y;
-        }
-        double a[3], d[3];
-#pragma unroll
-        for (int m = 0; m < 3; ++m)
-          fwd_pair<L, FMA>(tp, [&](int j) { return x[j + 2 * m]; }, a[m], d[m]);
-        asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(d[0]), "+v"(d[1]), "+v"(d[2])
-                     :: "memory");  // slot boundary
-        if constexpr (l == K) {
-          const int hp = h >> K;
-          double* pa = y + (int64_t)(2 * s) * hp + t * (T >> K) + i0;
-#pragma unroll
-          for (int m = 0; m < 3; ++m)
-            if (i0 + m < mo) {
-              pa[m] = a[m];
-              pa[hp + m] = d[m];
-            }
-        } else {
-#pragma unroll
-          for (int m = 0; m < 3; ++m) {
-            ra[r][m] = a[m];
-            rd[r][m] = d[m];
-          }
-        }
-      }
-    }
-    if constexpr (l < K) {
-      lds_barrier();
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int q = tid + r * NT;
-        if ((r + 1) * NT <= NC || q < NC) {
-          const int i0 = wo[r] % mo;  // == 3 * (q % N3): (2s)*mo is a multiple of mo
-#pragma unroll
-          for (int m = 0; m < 3; ++m)
-            if (i0 + m < mo) {
-              lds[wo[r] + m] = ra[r][m];
-              lds[wo[r] + mo + m] = rd[r][m];
-            }
-        }
-      }
-      lds_barrier();
-      Wpt1FwdLevel3<L, NT, T, K, FMA, l + 1>::run(tp, lds, h, t, y);
-    }
-  }
-};
-
-template <int L, int NT, int T, int K, bool FMA>
-__global__ __launch_bounds__(NT) void wpt_fwd_tile1t(const double* __restrict__ src, AxisView sv,
-                                                     double* __restrict__ dst, AxisView dv, int h,
-                                                     FwdTaps<L> tp) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  using G = Wpt1FwdGeo<L, T, K>;
-  constexpr int M0 = G::m(0);
-  const int ntile = h / T;
-  const int nblk = gridDim.x;
-  int b = blockIdx.x;
-  if ((nblk & 7) == 0) b = (b & 7) * (nblk >> 3) + (b >> 3);
-  const int t = b % ntile;
-  const int64_t o = b / ntile;
-  const double* s = src + view_base(sv, o);
-  const int msk = h - 1, base = t * T;
-  load_window<1, NT, (M0 + NT - 1) / NT>(lds, s, M0, true, 0, 1,
-                                          [&](int e) { return (int64_t)((base + e) & msk); });
-  dma_fence_barrier();
-  Wpt1FwdLevel3<L, NT, T, K, FMA, 1>::run(tp, lds, h, t, dst + view_base(dv, o));
+  Wpt1FwdLevel<L, NT, T, K, FMA, 1>::run(tp, lds, h, t, dst + view_base(dv, o));
 }
 
 // ---------------------------------------------------------------- reverse
@@ -283,8 +178,7 @@ __device__ __forceinline__ void rev_couple_ilv(const RevTaps<L>& tp, const doubl
   o1 = so1;
 }
 
-template <int L, int NT, int T, int K, bool FMA, int l, bool ILV = false, int DG = 0,
-          bool PAD = false>
+template <int L, int NT, int T, int K, bool FMA, int l, bool ILV = false, bool PAD = false>
 struct Wpt1RevLevel {
   // lds: 2^l packet windows of len(l) (stride len(l)); produces 2^(l-1)
   // windows of len(l-1) (level 1: the T outputs, to y).  Each lane computes
@@ -377,31 +271,21 @@ struct Wpt1RevLevel {
       for (int r = 0; r < R; ++r) {
         const int k = tid + r * NT;
         if ((r + 1) * NT <= NC || k < NC) {
-          if constexpr (DG == 1) {
-            // diagnostic (wrong results): the same two 16-B stores per couple
-            // at a 16-B lane stride into the first 4*NT doubles
-            *reinterpret_cast<double2*>(lds + 2 * tid) = make_double2(rx[r].x, rx[r].y);
-            *reinterpret_cast<double2*>(lds + 2 * (tid + NT)) = make_double2(rx[r].z, rx[r].w);
-          } else {
-            double* ob = lds + (wo[r] >> 2);
-            if (wo[r] & 1) *reinterpret_cast<double2*>(ob) = make_double2(rx[r].x, rx[r].y);
-            if (wo[r] & 2) *reinterpret_cast<double2*>(ob + 2) = make_double2(rx[r].z, rx[r].w);
-          }
+          double* ob = lds + (wo[r] >> 2);
+          if (wo[r] & 1) *reinterpret_cast<double2*>(ob) = make_double2(rx[r].x, rx[r].y);
+          if (wo[r] & 2) *reinterpret_cast<double2*>(ob + 2) = make_double2(rx[r].z, rx[r].w);
         }
       }
       if (hs >= 0) *reinterpret_cast<double2*>(lds + hs * lo_ + 2 * hml) = make_double2(hxe, hxo);
       lds_barrier();
-      Wpt1RevLevel<L, NT, T, K, FMA, l - 1, ILV, DG, PAD>::run(tp, lds, t, y);
+      Wpt1RevLevel<L, NT, T, K, FMA, l - 1, ILV, PAD>::run(tp, lds, t, y);
     }
   }
 };
 
 // Grid: rows * (h / T) blocks; h = output packet size of the pass; input
 // row o holds 2^K packets of h/2^K (view sv), output row o (view dv).
-// DMA = false: the windows through registers (diagnostic A/B of the LDS-DMA
-// load's share of the LDS counters)
-template <int L, int NT, int T, int K, bool FMA, bool ILV = false, bool DMA = true, int DG = 0,
-          bool PAD = false>
+template <int L, int NT, int T, int K, bool FMA, bool ILV = false, bool PAD = false>
 __global__ __launch_bounds__(NT) void wpt_rev_tile1(const double* __restrict__ src, AxisView sv,
                                                     double* __restrict__ dst, AxisView dv, int h,
                                                     RevTaps<L> tp) {
@@ -423,12 +307,12 @@ __global__ __launch_bounds__(NT) void wpt_rev_tile1(const double* __restrict__ s
   constexpr int SK = G::stride(K, PAD);
   static_assert(SK == LK, "level-K windows are contiguous");
   load_window<1, NT, (NW * SK + NT - 1) / NT>(
-      lds, s, NW * SK, DMA, 0, 1, [&](int e) {
+      lds, s, NW * SK, true, 0, 1, [&](int e) {
         const int w = e / SK, k = e - w * SK;
         return (int64_t)w * hp + ((BK + k) & pm);
       });
   dma_fence_barrier();
-  Wpt1RevLevel<L, NT, T, K, FMA, K, ILV, DG, PAD>::run(tp, lds, t, dst + view_base(dv, o));
+  Wpt1RevLevel<L, NT, T, K, FMA, K, ILV, PAD>::run(tp, lds, t, dst + view_base(dv, o));
 }
 
 }  // namespace jwv
