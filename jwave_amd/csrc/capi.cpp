@@ -22,6 +22,7 @@
 #include <condition_variable>
 #include <functional>
 #include <mutex>
+#include <sched.h>
 #include <thread>
 #include <string>
 #include <vector>
@@ -137,6 +138,7 @@ struct jwv_ctx {
   DevBuf red;    // reduction scratch (CompressorMagnitude)
   DevBuf hin, hout;  // device buffers of the host-pointer entry points
   PinRing pin;       // their pinned host staging (allocated on first use)
+  unsigned tail_calls = 0;  // fused forward tail launches (its counter slot)
   // single-launch FWT chains: [0, kWords) forward counters, [kWords, 2 kWords)
   // reverse ticket/flags; zeroed once, left zero by every completed launch
   unsigned* sync = nullptr;
@@ -356,14 +358,23 @@ bool fast1(const Bank& b, const Axis& a, bool rev) {
 // the whole level plan; everything else takes the multi-launch plan below.
 using jwv::ChainGeo;
 
+// [0, kWords) forward chain, [kWords, 2 kWords) reverse chain, then
+// kTailSlots arrival counters of the fused forward tail, one per call in
+// flight (call k uses slot k % kTailSlots; its last arriver re-zeroes it), so
+// tail launches queued on different streams of one context never share a
+// counter.
+constexpr int kTailSlots = 64;
+constexpr size_t kSyncWords = 2 * ChainGeo::kWords + 16 + kTailSlots;
 unsigned* sync_words(jwv_ctx* c) {
   if (!c->sync) {
-    // [0, kWords) forward chain, [kWords, 2 kWords) reverse chain, then the
-    // fused forward tail's counter (kTailWord)
-    HIPCHK(hipMalloc(&c->sync, (2 * ChainGeo::kWords + 16) * sizeof(unsigned)));
-    HIPCHK(hipMemsetAsync(c->sync, 0, (2 * ChainGeo::kWords + 16) * sizeof(unsigned), c->stream));
+    HIPCHK(hipMalloc(&c->sync, kSyncWords * sizeof(unsigned)));
+    HIPCHK(hipMemsetAsync(c->sync, 0, kSyncWords * sizeof(unsigned), c->stream));
   }
   return c->sync;
+}
+unsigned* tail_counter(jwv_ctx* c) {
+  unsigned* w = sync_words(c) + 2 * ChainGeo::kWords + 16;
+  return w + (c->tail_calls++ % kTailSlots);
 }
 
 int plan_of(jwv_ctx* c) { return c->plan >= 0 ? c->plan : ChainGeo::default_plan(); }
@@ -466,8 +477,7 @@ void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
     if (f1 && a.outer == 1 && h < a.len && (plan_of(c) & JWV_PLAN_FWD_TAIL) &&
         K >= jwv::kTailKMin && K <= jwv::kTailKMax && rem > K && h % jwv::kTailTB == 0 &&
         (h >> K) <= jwv::kTailCap && ((uintptr_t)cur & 15) == 0) {
-      jwv::TailArgs ta{cur, a.dst, c->ws[pp].p, sync_words(c) + 2 * ChainGeo::kWords, h, K,
-                       rem - K};
+      jwv::TailArgs ta{cur, a.dst, c->ws[pp].p, tail_counter(c), h, K, rem - K};
       { ProfScope ps_(c, K_FWT_FWD_TAIL, 16.0 * h);
         hipchk(use_fma(c) ? jwv::fused::fwt_fwd_tail(b, ta, c->stream)
                           : jwv::exact::fwt_fwd_tail(b, ta, c->stream), "fwt_fwd_tail"); }
@@ -799,8 +809,12 @@ PinRing& pin_ring(jwv_ctx* c) {
       hipchk(hipHostMalloc((void**)&r.p[i], kPinChunk, hipHostMallocDefault), "hipHostMalloc");
       hipchk(hipEventCreateWithFlags(&r.ev[i], hipEventDisableTiming), "hipEventCreate");
     }
-    const int hw = (int)std::thread::hardware_concurrency();
-    r.pool = new CopyPool(std::max(0, std::min(hw, 8) - 1));
+    // copy threads: the process's CPU share (sched affinity), at most 16
+    // (the GPU box's share per GPU), counting the caller
+    cpu_set_t cs;
+    int hw = (int)std::thread::hardware_concurrency();
+    if (sched_getaffinity(0, sizeof(cs), &cs) == 0) hw = CPU_COUNT(&cs);
+    r.pool = new CopyPool(std::max(0, std::min(hw, 16) - 1));
   }
   return r;
 }

@@ -5,6 +5,8 @@ set -o pipefail
 export JWAVE_AMD_NO_BUILD=1
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; mkdir -p gpurun_out
 T="timeout -k 10"
+$T 120 tools/diag/fp64_rate > gpurun_out/r04a_fp64_rate.txt 2>&1 || { cat gpurun_out/r04a_fp64_rate.txt; exit 1; }
+cat gpurun_out/r04a_fp64_rate.txt
 $T 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r04a_tests.txt 2>&1 || { tail -40 gpurun_out/r04a_tests.txt; exit 1; }
 tail -2 gpurun_out/r04a_tests.txt
 bash tools/gpu_ab_wl.sh modwt "JWV_MODWT_PIPE=0" "JWV_MODWT_PIPE=3" 3 > gpurun_out/r04a_pipe.txt 2>&1 || { cat gpurun_out/r04a_pipe.txt; exit 1; }
