@@ -1,6 +1,6 @@
 // launch_fwt8.hip — dispatch of the C = 8 column-slab tiles
 // (fwt8_kernels.hpp) for one math mode (compiled twice).
-#include "fwt8_kernels.hpp"
+#include "fwt16_kernels.hpp"
 #include <cstdlib>
 #include "jwv_launch.hpp"
 
@@ -52,8 +52,56 @@ hipError_t rev8_k(const Bank& b, const TileArgs& a, hipStream_t s) {
                      a.inner, tp, Geo::slab_order());
   return hipGetLastError();
 }
+// ---- C = 16 column slabs (fwt16_kernels.hpp): whole 128-B row lines.
+// Forward 512-row tiles (78 KB of LDS at L = 16: 2 blocks per CU), reverse
+// 256-row tiles (every window in LDS: 61 KB).  env JWV_FWT16=1 (A/B).
+constexpr int kT16F = 512, kT16R = 256;
+bool fwt16_env() {
+  static const bool v = [] {
+    const char* e = std::getenv("JWV_FWT16");
+    return e && std::atoi(e) != 0;
+  }();
+  return v;
+}
+template <int L, int K>
+hipError_t fwd16_k(const Bank& b, const TileArgs& a, hipStream_t s) {
+  auto k = fwt_fwd_tile16<L, 256, kT16F, K, kFMA>;
+  const size_t lds = (size_t)Fwd16Geo<L, kT16F, K>::lds_doubles() * sizeof(double);
+  if (hipError_t e = prep1(k, lds)) return e;
+  FwdTaps<L> tp;
+  for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
+  const dim3 grid((unsigned)(a.nouter * (a.inner / 16) * (a.h / kT16F)));
+  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a.src, a.sv, a.dst, a.dv, a.adst, a.av, a.h,
+                     a.inner, tp, Geo::slab_order());
+  return hipGetLastError();
+}
+template <int L, int K>
+hipError_t rev16_k(const Bank& b, const TileArgs& a, hipStream_t s) {
+  auto k = fwt_rev_tile16<L, 256, kT16R, K, kFMA>;
+  const size_t lds = (size_t)Rev16Geo<L, kT16R, K>::lds_doubles() * sizeof(double);
+  if (hipError_t e = prep1(k, lds)) return e;
+  RevTaps<L> tp;
+  for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
+  const int hK = a.h << (a.K - 1);
+  const dim3 grid((unsigned)(a.nouter * (a.inner / 16) * (hK / kT16R)));
+  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a.src, a.sv, a.coef, a.cv, a.dst, a.dv, hK,
+                     a.inner, tp, Geo::slab_order());
+  return hipGetLastError();
+}
+template <int L>
+hipError_t tile16_l(const Bank& b, const TileArgs& a, hipStream_t s, bool fwd) {
+  switch (a.K) {
+    case 1: return fwd ? fwd16_k<L, 1>(b, a, s) : rev16_k<L, 1>(b, a, s);
+    case 2: return fwd ? fwd16_k<L, 2>(b, a, s) : rev16_k<L, 2>(b, a, s);
+    default: return fwd ? fwd16_k<L, 3>(b, a, s) : rev16_k<L, 3>(b, a, s);
+  }
+}
 template <int L>
 hipError_t tile8_l(const Bank& b, const TileArgs& a, hipStream_t s, bool fwd) {
+  if (a.inner % 16 == 0 && fwt16_env()) {
+    const int64_t hT = fwd ? (int64_t)a.h : ((int64_t)a.h << (a.K - 1));
+    if (hT % (fwd ? kT16F : kT16R) == 0) return tile16_l<L>(b, a, s, fwd);
+  }
   switch (a.K) {
     case 1: return fwd ? fwd8_k<L, 1>(b, a, s) : rev8_k<L, 1>(b, a, s);
     case 2: return fwd ? fwd8_k<L, 2>(b, a, s) : rev8_k<L, 2>(b, a, s);

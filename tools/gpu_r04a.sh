@@ -15,3 +15,5 @@ bash tools/gpu_kstats.sh r04a_ks_modwt modwt > gpurun_out/r04a_ks_modwt.txt 2>&1
 cat gpurun_out/r04a_ks_modwt.txt
 bash tools/gpu_ab_wl.sh wpt "JWV_WPT_PAD=0" "JWV_WPT_PAD=1" 2 "wpt_config4 or wpt_large" > gpurun_out/r04a_pad.txt 2>&1 || { cat gpurun_out/r04a_pad.txt; exit 1; }
 cat gpurun_out/r04a_pad.txt
+bash tools/gpu_ab_wl.sh fwt2d "JWV_FWT16=0" "JWV_FWT16=1" 2 "fwt2d or 3d or axis_columns or parallel_transform" > gpurun_out/r04a_fwt16.txt 2>&1 || { cat gpurun_out/r04a_fwt16.txt; exit 1; }
+cat gpurun_out/r04a_fwt16.txt
