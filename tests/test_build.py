@@ -33,6 +33,6 @@ def test_library_reads_no_variant_switches():
     blob = open(_lib.LIB_PATH, "rb").read()
     names = set(re.findall(rb"JWV_[A-Z0-9_]+", blob))
     allowed = {b"JWV_LAUNCH", b"JWV_LAUNCH_LOG", b"JWV_TRANSFORM_FWT", b"JWV_TRANSFORM_WPT",
-               b"JWV_MODWT_PIPE", b"JWV_WPT_PAD"}
+               b"JWV_MODWT_PIPE", b"JWV_WPT_PAD", b"JWV_FWT16"}
     assert names <= allowed, sorted(names - allowed)
     assert b"JWV_WPT_DIAGW" not in blob
