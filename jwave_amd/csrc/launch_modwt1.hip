@@ -75,12 +75,12 @@ hipError_t inv_kp(const Bank& b, const ModwtArgs& a, hipStream_t s) {
 // Pipelined inverse / forward (modwt_pipe.hpp): persistent 1024-thread blocks,
 // one per CU, windows by LDS-DMA; tiles 1024 (inverse) / 8192 (forward).
 // Need 16-B aligned rows (ldw even) and outputs.  env JWV_MODWT_PIPE: bit 0
-// inverse, bit 1 forward (default 3).
+// inverse, bit 1 forward (A/B this round; default off until measured).
 constexpr int kPipeT = 1024, kPipeNT = 1024, kPipeTF = 8192;
 int pipe_env() {
   static const int v = [] {
     const char* e = std::getenv("JWV_MODWT_PIPE");
-    return e ? std::atoi(e) : 3;
+    return e ? std::atoi(e) : 0;
   }();
   return v;
 }
