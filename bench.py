@@ -558,6 +558,15 @@ def secondary_wpt(args, d):
     return out
 
 
+def _copy_threads():
+    """Threads of the library's host copy pool: the process's CPU share, at
+    most 16 (capi.cpp pin_ring)."""
+    try:
+        return min(len(os.sched_getaffinity(0)), 16)
+    except Exception:
+        return min(os.cpu_count() or 1, 16)
+
+
 def host_entry(args, d, reps=5):
     """SURVEY 8(d) secondary reporting: the drop-in host path end to end
     (Transform.forward(double[]) -> FastWaveletTransform, Transform.java:81-90):
@@ -596,7 +605,20 @@ def host_entry(args, d, reps=5):
 
     out = {"workload": "config 2 (D4, N=2^24, full depth) through the host-pointer entries, "
                        "forward + reverse per step", "steps": reps}
+    st = (ctypes.c_double * 6)()
+    step(x, y, xr)  # first touch of the outputs, ring allocation
+    lib.jwv_ctx_stage_stats(h, st, 1)
     out["pageable_ms_per_step"] = round(per_step(lambda: step(x, y, xr)), 3)
+    lib.jwv_ctx_stage_stats(h, st, 1)
+    nst = reps + 1  # per_step runs one untimed call first
+    # the pinned ring (capi.cpp PinRing): host copy threads, their time and
+    # the time they waited for the DMA engine, per step; overlap = the share
+    # of the host copies that ran while a DMA was in flight
+    cp = (st[0] + st[3]) / nst * 1e3
+    wt = (st[1] + st[2]) / nst * 1e3
+    out["ring"] = {"copy_threads": _copy_threads(), "host_copy_ms_per_step": round(cp, 3),
+                   "dma_wait_ms_per_step": round(wt, 3),
+                   "bytes_per_step": (st[4] + st[5]) / nst}
     err = float(np.abs(xr - x).max())
     bufs = [ctypes.c_void_p() for _ in range(3)]
     try:

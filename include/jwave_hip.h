@@ -132,6 +132,12 @@ int jwv_ctx_trim(jwv_ctx* ctx);
  * GPU work.  No Java counterpart (boundary plumbing). */
 int jwv_host_alloc(jwv_ctx* ctx, int64_t bytes, void** p);
 int jwv_host_free(jwv_ctx* ctx, void* p);
+/* Cumulative seconds the context's host entries spent staging pageable
+ * arrays: out[0] host copies into the pinned ring, out[1] waits for a ring
+ * slot's H2D DMA, out[2] waits for a slot's D2H DMA, out[3] host copies out
+ * of the ring, out[4] bytes staged in, out[5] bytes staged out.  reset != 0
+ * zeroes them after reading.  Diagnostic (bench.py's host_entry object). */
+int jwv_ctx_stage_stats(jwv_ctx* ctx, double* out6, int reset);
 int jwv_version(void);
 
 /* ---- 1-D FWT ---------------------------------------------------------------

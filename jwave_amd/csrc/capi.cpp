@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -121,7 +122,11 @@ struct PinRing {
   char* p[kPinSlots] = {};
   hipEvent_t ev[kPinSlots] = {};
   CopyPool* pool = nullptr;
+  double stat[6] = {};  // jwv_ctx_stage_stats
 };
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 }  // namespace
 
@@ -830,11 +835,16 @@ void copy_in(jwv_ctx* c, const double* x, double* dx, size_t n) {
   for (size_t off = 0, k = 0; off < bytes; off += kPinChunk, ++k) {
     const int s = (int)(k % kPinSlots);
     const size_t len = std::min(kPinChunk, bytes - off);
+    const double t0 = now_s();
     hipchk(hipEventSynchronize(r.ev[s]), "staging slot");  // its previous DMA is done
+    const double t1 = now_s();
     r.pool->copy(r.p[s], (const char*)x + off, len);
+    r.stat[1] += t1 - t0;
+    r.stat[0] += now_s() - t1;
     hipchk(hipMemcpyAsync((char*)dx + off, r.p[s], len, hipMemcpyHostToDevice, c->stream), "H2D");
     hipchk(hipEventRecord(r.ev[s], c->stream), "hipEventRecord");
   }
+  r.stat[4] += (double)bytes;
 }
 
 // device dy -> host y, after the queued work; returns when y is complete
@@ -858,10 +868,15 @@ void copy_out(jwv_ctx* c, const double* dy, double* y, size_t n) {
   for (size_t k = 0; k < nk; ++k) {
     const int s = (int)(k % kPinSlots);
     const size_t off = k * kPinChunk, len = std::min(kPinChunk, bytes - off);
+    const double t0 = now_s();
     hipchk(hipEventSynchronize(r.ev[s]), "staging slot");
+    const double t1 = now_s();
     r.pool->copy((char*)y + off, r.p[s], len);
+    r.stat[2] += t1 - t0;
+    r.stat[3] += now_s() - t1;
     if (k + kPinSlots < nk) issue(k + kPinSlots);
   }
+  r.stat[5] += (double)bytes;
   hipchk(hipStreamSynchronize(c->stream), "sync");
 }
 
@@ -1291,6 +1306,14 @@ int jwv_host_free(jwv_ctx* c, void* p) {
   return guarded(c, [&] {
     if (p) hipchk(hipHostFree(p), "hipHostFree");
   });
+}
+
+int jwv_ctx_stage_stats(jwv_ctx* c, double* out, int reset) {
+  if (!c || !out) return set_err(c, JWV_ERR_BAD_CALL, "jwv_ctx_stage_stats: NULL argument");
+  for (int i = 0; i < 6; ++i) out[i] = c->pin.stat[i];
+  if (reset)
+    for (int i = 0; i < 6; ++i) c->pin.stat[i] = 0.0;
+  return JWV_OK;
 }
 
 int jwv_ctx_destroy(jwv_ctx* c) {
