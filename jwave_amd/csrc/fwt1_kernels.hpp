@@ -236,6 +236,10 @@ struct Rev1Level {
             dv[j] = w.x;
             dv[j + 1] = w.y;
           }
+          // window in registers here (else the loads sink into rev_pair's
+          // term loop as ds_read2_b64 at odd offsets, see wpt1_kernels.hpp)
+#pragma unroll
+          for (int j = 0; j < NR; ++j) asm volatile("" : "+v"(av[j]), "+v"(dv[j]));
           // pair ml reads a[li - q] = av[(Q-1) + sh - q]; pair ml+1 one further
           double x0e, x0o, x1e, x1o;
           rev_pair<L, FMA>(tp, av + (Q - 1) + sh, dv + (Q - 1) + sh, 1, x0e, x0o);

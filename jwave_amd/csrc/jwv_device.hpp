@@ -357,6 +357,17 @@ __device__ __forceinline__ void poll_all(const unsigned* f, int n, unsigned v, u
   if (lane == 0) store_agent(tmo, 1u);
 }
 
+// 16-B LDS read at a 16-B aligned address the compiler cannot prove aligned
+// on its own (offsets built from runtime lane indices): without the
+// assumption it splits the access into ds_read2_b64 (8 cycles, and 2-way
+// bank-conflicted at a 16-B lane stride) instead of one ds_read_b128.
+__device__ __forceinline__ double2 ld16(const double* p) {
+  return *reinterpret_cast<const double2*>(__builtin_assume_aligned(p, 16));
+}
+__device__ __forceinline__ void st16(double* p, double a, double b) {
+  *reinterpret_cast<double2*>(__builtin_assume_aligned(p, 16)) = make_double2(a, b);
+}
+
 // Materialise two results here: stops the compiler from sinking their
 // computation into later exec-masked stores, where two independent FP64
 // accumulation chains would run one after the other instead of interleaved

@@ -163,6 +163,9 @@ struct InvPipe {
           aw1[l] = z.y;
         }
       }
+#pragma unroll
+      for (int l = 0; l < L; ++l)
+        asm volatile("" : "+v"(av0[l]), "+v"(av1[l]), "+v"(aw0[l]), "+v"(aw1[l]));
       double sa0 = 0.0, sd0 = 0.0, sa1 = 0.0, sd1 = 0.0;
 #pragma unroll
       for (int l = 0; l < L; ++l) {
@@ -375,6 +378,8 @@ struct FwdPipe {
           v[i + 1] = u.y;
         }
 #pragma unroll
+        for (int i = 0; i < L + 2; ++i) asm volatile("" : "+v"(v[i]));
+#pragma unroll
         for (int l = 0; l < L; ++l) {
           x0[l] = v[L - l];
           x1[l] = v[L + 1 - l];
@@ -387,6 +392,9 @@ struct FwdPipe {
           x1[l] = u.y;
         }
       }
+      // operands in registers here (16-B ds_read_b128, not per-use reads)
+#pragma unroll
+      for (int l = 0; l < L; ++l) asm volatile("" : "+v"(x0[l]), "+v"(x1[l]));
       double sw0 = 0.0, sv0 = 0.0, sw1 = 0.0, sv1 = 0.0;
 #pragma unroll
       for (int l = 0; l < L; ++l) {

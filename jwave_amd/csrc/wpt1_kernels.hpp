@@ -220,11 +220,16 @@ struct Wpt1RevLevel {
         double av[NR], dv[NR];
 #pragma unroll
         for (int j = 0; j < NR; j += 2) {
-          const double2 u = *reinterpret_cast<const double2*>(ab + st + j);
-          const double2 w = *reinterpret_cast<const double2*>(db + st + j);
+          const double2 u = ld16(ab + st + j);
+          const double2 w = ld16(db + st + j);
           av[j] = u.x; av[j + 1] = u.y;
           dv[j] = w.x; dv[j + 1] = w.y;
         }
+        // the window in registers here: left to itself the compiler sinks
+        // the loads into the term loop as per-term ds_read2_b64 at odd
+        // offsets (8 cycles each, 2-way conflicted), not 16-B ds_read_b128
+#pragma unroll
+        for (int j = 0; j < NR; ++j) asm volatile("" : "+v"(av[j]), "+v"(dv[j]));
         // pair ml: a[li - q] = av[(Q-1) + sh - q]; pair ml+1: one further
         double x0e, x0o, x1e, x1o;
         if constexpr (ILV) {

@@ -15,7 +15,7 @@ natives would be called (HipNative.java:92-124):
 * GPU: the same shim on the real library: Transform.forward(double[])'s
   drop-in path (Transform.java:81-90 -> HipFastWaveletTransform ->
   HipNative.transform1d) is bit-identical to the oracle, and the reference's
-  level error reaches Java as status 2 + lastError text.
+  level error reaches Java as status 1 (JWaveFailure) + lastError text.
 """
 import ctypes
 import os
@@ -337,7 +337,7 @@ def test_real_library_links_and_reports_no_device():
 def test_real_library_drop_in_path_gpu():
     """HipFastWaveletTransform.forward/reverse(double[]) and HipMODWTTransform
     through the shim on the GPU: bit-identical to the oracle; the reference's
-    level error arrives as ILLEGAL_ARGUMENT + its message."""
+    level error arrives as FAILURE (JWaveFailure) + its message."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     so = os.path.join(JNI, "build", "libjni_real.so")
@@ -363,7 +363,7 @@ def test_real_library_drop_in_path_gpu():
     assert j.native("modwt", ctx, 1, jm, jwv, m, Jl, *tp) == 0
     assert np.array_equal(j.read(jwv, (Jl + 1) * m).reshape(Jl + 1, m),
                           oracle.modwt_forward(w, x[:m], Jl))
-    # level beyond log2 n: the reference's IllegalArgument path
-    assert j.native("transform1d", ctx, 0, 1, jx, jy, 17, *j.taps(w)) == 2
+    # level beyond log2 n: FastWaveletTransform.java:80-83's JWaveFailure
+    assert j.native("transform1d", ctx, 0, 1, jx, jy, 17, *j.taps(w)) == 1
     assert j.lib.fj_string(j.native("lastError", ctx))
     j.free_all()
