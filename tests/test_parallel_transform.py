@@ -112,4 +112,6 @@ def test_parallel_transform_gpu_parity(kind, name):
     ref = _axis(kind, False, w, ref, 2, lq)
     got = pt.reverse(f, lp, lq, lr)
     assert np.array_equal(got, ref)
-    assert np.abs(got - s).max() < 1e-12
+    # a round trip at partial levels in a different axis order than the
+    # forward: exact in real arithmetic, ~1e-11 in doubles (not a parity claim)
+    assert np.abs(got - s).max() < 1e-9
