@@ -1068,7 +1068,7 @@ void check_modwt(int64_t n, int J) {
   }
 }
 
-// The compile-time-geometry MODWT tiles (modwt1_kernels.hpp, modwt_pipe.hpp)
+// The compile-time-geometry MODWT tiles (modwt1_kernels.hpp)
 // where they cover the case, else the runtime tiles.
 bool modwt_ct() { return true; }
 

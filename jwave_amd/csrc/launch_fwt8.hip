@@ -1,7 +1,6 @@
 // launch_fwt8.hip — dispatch of the C = 8 column-slab tiles
 // (fwt8_kernels.hpp) for one math mode (compiled twice).
 #include "fwt16_kernels.hpp"
-#include <cstdlib>
 #include "jwv_launch.hpp"
 
 #ifndef JWV_FMA
@@ -54,15 +53,9 @@ hipError_t rev8_k(const Bank& b, const TileArgs& a, hipStream_t s) {
 }
 // ---- C = 16 column slabs (fwt16_kernels.hpp): whole 128-B row lines.
 // Forward 512-row tiles (78 KB of LDS at L = 16: 2 blocks per CU), reverse
-// 256-row tiles (every window in LDS: 61 KB).  env JWV_FWT16=1 (A/B).
+// 256-row tiles (every window in LDS: 61 KB).  Config 3 against the C = 8
+// tiles (r04b, one box, two rounds): 1.368 / 1.371 -> 1.341 / 1.334 ms/step.
 constexpr int kT16F = 512, kT16R = 256;
-bool fwt16_env() {
-  static const bool v = [] {
-    const char* e = std::getenv("JWV_FWT16");
-    return e && std::atoi(e) != 0;
-  }();
-  return v;
-}
 template <int L, int K>
 hipError_t fwd16_k(const Bank& b, const TileArgs& a, hipStream_t s) {
   auto k = fwt_fwd_tile16<L, 256, kT16F, K, kFMA>;
@@ -98,7 +91,7 @@ hipError_t tile16_l(const Bank& b, const TileArgs& a, hipStream_t s, bool fwd) {
 }
 template <int L>
 hipError_t tile8_l(const Bank& b, const TileArgs& a, hipStream_t s, bool fwd) {
-  if (a.inner % 16 == 0 && fwt16_env()) {
+  if (a.inner % 16 == 0) {
     const int64_t hT = fwd ? (int64_t)a.h : ((int64_t)a.h << (a.K - 1));
     if (hT % (fwd ? kT16F : kT16R) == 0) return tile16_l<L>(b, a, s, fwd);
   }

@@ -1,7 +1,6 @@
 // launch_wpt1.hip — dispatch of the C = 1 compile-time-geometry WPT tiles
 // (wpt1_kernels.hpp) for one math mode (compiled twice).
 #include "wpt1_kernels.hpp"
-#include <cstdlib>
 #include "jwv_launch.hpp"
 
 #ifndef JWV_FMA
@@ -37,24 +36,13 @@ hipError_t wfwd1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a.src, a.sv, a.dst, a.dv, a.h, tp);
   return hipGetLastError();
 }
-// env JWV_WPT_PAD=1: the config-4 reverse tile with padded window strides
-// (conflict-free reads across window boundaries by the bank model)
-bool wpt_pad() {
-  static const bool v = [] {
-    const char* e = std::getenv("JWV_WPT_PAD");
-    return e && std::atoi(e) != 0;
-  }();
-  return v;
-}
 // The reverse tiles' couples as four interleaved sums (rev_couple_ilv) for
 // L >= 8: config 4 reverse 2728-2752 -> 2702-2708 us.
 template <int L, int K>
 hipError_t wrev1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
   constexpr bool ILV = L >= 8;
-  const bool pad = ILV && L == 16 && K == 6 && wpt_pad();
-  auto k = pad ? wpt_rev_tile1<L, 256, kWptT, K, kFMA, ILV, true>
-               : wpt_rev_tile1<L, 256, kWptT, K, kFMA, ILV, false>;
-  const size_t lds = (size_t)Wpt1RevGeo<L, kWptT, K>::lds_doubles(pad) * sizeof(double);
+  auto k = wpt_rev_tile1<L, 256, kWptT, K, kFMA, ILV>;
+  const size_t lds = (size_t)Wpt1RevGeo<L, kWptT, K>::lds_doubles() * sizeof(double);
   if (hipError_t e = prep1(k, lds)) return e;
   RevTaps<L> tp;
   for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }

@@ -124,30 +124,6 @@ struct Wpt1RevGeo {
   static constexpr int c(int l) { return R::c(l); }
   // + 4: the odd-window couple tail reads up to two samples past a window
   static constexpr int lds_doubles() { return (1 << K) * len(K) + 4; }
-  // Padded window stride of level l (PAD): couples of consecutive output
-  // windows then continue the 16-B slot sequence mod 16 across a window
-  // boundary (lane k+1 lands stride - (ncw - 1) slots after lane k: 1 mod 16
-  // for an even couple count; for an odd one the even stride allows 2 mod 16,
-  // one 2-way slot per straddling group), so a ds_read_b128 lane group
-  // straddling a boundary stays (nearly) conflict-free
-  // (tools/wpt_rev_bank_model.py).  Strides stay even: the d window sits one
-  // stride after its a window and must stay 16-B aligned.
-  static constexpr int ncw(int l) { return (len(l - 1) / 2 + 1) / 2; }
-  // Level K (the DMA'd windows, the largest level in LDS) stays unpadded so
-  // the block keeps its LDS size (config 4: 4 blocks per CU).
-  static constexpr int stride(int l, bool pad) {
-    if (!pad || l < 1 || l >= K) return len(l);
-    const int want = (ncw(l) + (ncw(l) & 1)) % 16;  // even residue
-    int st = len(l);
-    while (st % 16 != want) st += 2;  // len(l) is even
-    return st;
-  }
-  static constexpr int lds_doubles(bool pad) {
-    if (!pad) return lds_doubles();
-    int b = 0;
-    for (int l = 1; l <= K; ++l) b = (1 << l) * stride(l, true) > b ? (1 << l) * stride(l, true) : b;
-    return b + 4;
-  }
 };
 
 // Couple (pairs m, m+1) of rev_pair with the term loop shared: A/D point at
@@ -178,7 +154,7 @@ __device__ __forceinline__ void rev_couple_ilv(const RevTaps<L>& tp, const doubl
   o1 = so1;
 }
 
-template <int L, int NT, int T, int K, bool FMA, int l, bool ILV = false, bool PAD = false>
+template <int L, int NT, int T, int K, bool FMA, int l, bool ILV = false>
 struct Wpt1RevLevel {
   // lds: 2^l packet windows of len(l) (stride len(l)); produces 2^(l-1)
   // windows of len(l-1) (level 1: the T outputs, to y).  Each lane computes
@@ -192,8 +168,7 @@ struct Wpt1RevLevel {
                                              double* __restrict__ y) {
     using G = Wpt1RevGeo<L, T, K>;
     constexpr int Q = L / 2;
-    // window strides in LDS (PAD: padded, see Wpt1RevGeo::stride)
-    constexpr int li_ = G::stride(l, PAD), lo_ = G::stride(l - 1, PAD);
+    constexpr int li_ = G::len(l), lo_ = G::len(l - 1);  // window strides in LDS
     constexpr int NW = 1 << (l - 1);                // output windows
     constexpr int NPW = G::len(l - 1) / 2;          // pairs per output window
     constexpr int NCW = (NPW + 1) / 2;              // couples per output window
@@ -283,14 +258,14 @@ struct Wpt1RevLevel {
       }
       if (hs >= 0) *reinterpret_cast<double2*>(lds + hs * lo_ + 2 * hml) = make_double2(hxe, hxo);
       lds_barrier();
-      Wpt1RevLevel<L, NT, T, K, FMA, l - 1, ILV, PAD>::run(tp, lds, t, y);
+      Wpt1RevLevel<L, NT, T, K, FMA, l - 1, ILV>::run(tp, lds, t, y);
     }
   }
 };
 
 // Grid: rows * (h / T) blocks; h = output packet size of the pass; input
 // row o holds 2^K packets of h/2^K (view sv), output row o (view dv).
-template <int L, int NT, int T, int K, bool FMA, bool ILV = false, bool PAD = false>
+template <int L, int NT, int T, int K, bool FMA, bool ILV = false>
 __global__ __launch_bounds__(NT) void wpt_rev_tile1(const double* __restrict__ src, AxisView sv,
                                                     double* __restrict__ dst, AxisView dv, int h,
                                                     RevTaps<L> tp) {
@@ -307,17 +282,14 @@ __global__ __launch_bounds__(NT) void wpt_rev_tile1(const double* __restrict__ s
   const double* s = src + view_base(sv, o);
   const int hp = h >> K, pm = hp - 1;
   const int BK = t * (T >> K) - G::c(K);
-  // all 2^K packet windows in one burst: window w -> lds[w * SK ..) (level K
-  // is never padded: SK = LK)
-  constexpr int SK = G::stride(K, PAD);
-  static_assert(SK == LK, "level-K windows are contiguous");
-  load_window<1, NT, (NW * SK + NT - 1) / NT>(
-      lds, s, NW * SK, true, 0, 1, [&](int e) {
-        const int w = e / SK, k = e - w * SK;
+  // all 2^K packet windows in one burst: window w -> lds[w * LK ..)
+  load_window<1, NT, (NW * LK + NT - 1) / NT>(
+      lds, s, NW * LK, true, 0, 1, [&](int e) {
+        const int w = e / LK, k = e - w * LK;
         return (int64_t)w * hp + ((BK + k) & pm);
       });
   dma_fence_barrier();
-  Wpt1RevLevel<L, NT, T, K, FMA, K, ILV, PAD>::run(tp, lds, t, dst + view_base(dv, o));
+  Wpt1RevLevel<L, NT, T, K, FMA, K, ILV>::run(tp, lds, t, dst + view_base(dv, o));
 }
 
 }  // namespace jwv

@@ -59,69 +59,3 @@ def test_even_m_would_conflict():
     grp = B128_GROUPS[0]
     slots = [slot0(lane, 2, 2)[0] % 16 for lane in grp]
     assert len(set(slots)) < 16
-
-
-# ---------------------------------------------------------------------------
-# WPT reverse tile (wpt1_kernels.hpp, Wpt1RevLevel / Wpt1RevGeo::stride):
-# couple k of level l reads slot s*stride(l) + (k % ncw) + const of its a/d
-# windows, s = k // ncw.  With the padded strides (levels 1..K-1), a 16-lane
-# ds_read_b128 group that straddles a window boundary keeps distinct slots
-# mod 16 (an even couple count) or at most one 2-way slot (an odd one).
-WL, WQ, WT, WK, WNT = 16, 8, 4096, 6, 256
-
-
-def _c(l):
-    cc = 0
-    for _ in range(l):
-        cc = ((cc // 2 + (WQ - 1)) + 1) & ~1
-    return cc
-
-
-def _len(l):
-    return (WT >> l) + _c(l)
-
-
-def _ncw(l):
-    return (_len(l - 1) // 2 + 1) // 2
-
-
-def _stride(l, pad):
-    if not pad or l < 1 or l >= WK:
-        return _len(l)
-    want = (_ncw(l) + (_ncw(l) & 1)) % 16
-    st = _len(l)
-    while st % 16 != want:
-        st += 2
-    return st
-
-
-def _max_extra(l, pad):
-    from collections import Counter
-    ncw, nc = _ncw(l), (1 << (l - 1)) * _ncw(l)
-    worst = 0
-    for k0 in range(0, nc, 64):
-        for grp in B128_GROUPS:
-            sl = [((k // ncw) * _stride(l, pad) + k % ncw) % 16
-                  for k in (k0 + g for g in grp) if k < nc]
-            if sl:
-                worst = max(worst, max(Counter(sl).values()) - 1)
-    return worst
-
-
-def test_wpt_padded_strides_keep_lds_size():
-    """Level K stays unpadded, so the block's LDS (4 blocks per CU) is unchanged."""
-    unpadded = (1 << WK) * _len(WK)
-    padded = max((1 << l) * _stride(l, True) for l in range(1, WK + 1))
-    assert padded == unpadded
-    for l in range(1, WK + 1):
-        assert _stride(l, True) % 2 == 0 and _stride(l, True) >= _len(l)
-
-
-@pytest.mark.parametrize("l", range(1, WK))
-def test_wpt_padded_reads_conflict_free(l):
-    assert _max_extra(l, True) <= (1 if _ncw(l) % 2 else 0)
-
-
-def test_wpt_unpadded_deep_levels_conflict():
-    """What the padding removes: unpadded window boundaries collide (levels 4, 5)."""
-    assert _max_extra(5, False) >= 1 and _max_extra(4, False) >= 1
