@@ -25,6 +25,26 @@ namespace jwv {
 #define JWV_MOD1_FENCE 2
 #endif
 
+// Diagnostic builds only (tools/diag/diag_modwt.hip; wrong results by design,
+// never defined for the library): JWV_EXP_MOD_NOBAR drops the level barriers,
+// JWV_EXP_MOD_NOWF the inverse's W fetches, JWV_EXP_MOD_NOFP the FP64 sums
+// (the LDS reads stay, combined by an integer xor).
+#ifdef JWV_EXP_MOD_NOBAR
+#define JWV_MOD_BAR() ((void)0)
+#else
+#define JWV_MOD_BAR() lds_barrier()
+#endif
+template <bool FMA>
+__device__ __forceinline__ double mod_mac(double acc, double a, double b) {
+#ifdef JWV_EXP_MOD_NOFP
+  (void)b;
+  return __builtin_bit_cast(double, __builtin_bit_cast(unsigned long long, acc) ^
+                                        __builtin_bit_cast(unsigned long long, a));
+#else
+  return mac<FMA>(acc, a, b);
+#endif
+}
+
 // Buffer-resource access for tiles that do not wrap: the block-uniform base
 // lives in SGPRs, a lane adds one 32-bit offset, slot offsets are scalar, so a
 // load or store costs no per-access 64-bit address VALU.
@@ -165,10 +185,10 @@ struct ModFwd1Level {
       double sw0 = 0.0, sv0 = 0.0, sw1 = 0.0, sv1 = 0.0;
 #pragma unroll
       for (int l = 0; l < L; ++l) {
-        sw0 = mac<FMA>(sw0, x0[l], tp.h[l]);
-        sv0 = mac<FMA>(sv0, x0[l], tp.g[l]);
-        sw1 = mac<FMA>(sw1, x1[l], tp.h[l]);
-        sv1 = mac<FMA>(sv1, x1[l], tp.g[l]);
+        sw0 = mod_mac<FMA>(sw0, x0[l], tp.h[l]);
+        sv0 = mod_mac<FMA>(sv0, x0[l], tp.g[l]);
+        sw1 = mod_mac<FMA>(sw1, x1[l], tp.h[l]);
+        sv1 = mod_mac<FMA>(sv1, x1[l], tp.g[l]);
       }
       pin2(sw0, sv0);
       pin2(sw1, sv1);
@@ -189,14 +209,14 @@ struct ModFwd1Level {
         if ((r + 1) % JWV_MOD1_FENCE == 0)
           asm volatile("" : "+v"(vv[r].x), "+v"(vv[r].y) :: "memory");
     }
-    lds_barrier();
+    JWV_MOD_BAR();
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int k = tid + r * NT;
       if ((r + 1) * NT <= NP || k < NP)
         *reinterpret_cast<double2*>(lds + kPad + e0 + 2 * k) = vv[r];
     }
-    lds_barrier();
+    JWV_MOD_BAR();
     if constexpr (j < J1)
       ModFwd1Level<L, NT, T, J0, J1, FMA, j + 1, P2, M>::run(tp, lds, wout, ldw, t0, N);
   }
@@ -226,7 +246,7 @@ __global__ __launch_bounds__(NT) void modwt_fwd_tile1(const double* __restrict__
   else
     load_window<1, NT, MAXP>(lds + pad, src, G::W, false, 0, 1,
                              [&](int e) { return wrap_mod(t0 - G::S + e, N); });
-  lds_barrier();
+  JWV_MOD_BAR();
   ModFwd1Level<L, NT, T, J0, J1, FMA, J0, P2, M>::run(tp, lds, wout, ldw, t0, N);
   const int tid = threadIdx.x;
 #pragma unroll
@@ -284,6 +304,11 @@ struct ModInv1Level {
     constexpr int Wn = T + G::Rin(j);
     const double* row = coef + (int64_t)(j - 1) * ldw;
     const int tid = opaque_tid();
+#ifdef JWV_EXP_MOD_NOWF
+#pragma unroll
+    for (int r = 0; r < MAXP; ++r) pw[r] = (double)(r + tid);
+    return;
+#endif
     if (inside) {
       // buffer loads: block-uniform base in SGPRs, one lane offset, the slot
       // offsets r*NT*8 as scalar offsets (no per-load 64-bit address VALU)
@@ -316,7 +341,7 @@ struct ModInv1Level {
       const int q = tid + r * NT;
       if (r * NT < Wn && ((r + 1) * NT <= Wn || q < Wn)) wb[q] = pw[r];
     }
-    lds_barrier();
+    JWV_MOD_BAR();
     if constexpr (j > J0)
       ModInv1Level<L, NT, T, J0, J1, FMA, j - 1, P2, M>::fetch(pw, coef, ldw, t0, N, inside);
     if constexpr (kRun)
@@ -379,10 +404,10 @@ struct ModInv1Level {
       double sa0 = 0.0, sd0 = 0.0, sa1 = 0.0, sd1 = 0.0;
 #pragma unroll
       for (int l = 0; l < L; ++l) {
-        sa0 = mac<FMA>(sa0, av0[l], tp.g[l]);
-        sd0 = mac<FMA>(sd0, aw0[l], tp.h[l]);
-        sa1 = mac<FMA>(sa1, av1[l], tp.g[l]);
-        sd1 = mac<FMA>(sd1, aw1[l], tp.h[l]);
+        sa0 = mod_mac<FMA>(sa0, av0[l], tp.g[l]);
+        sd0 = mod_mac<FMA>(sd0, aw0[l], tp.h[l]);
+        sa1 = mod_mac<FMA>(sa1, av1[l], tp.g[l]);
+        sd1 = mod_mac<FMA>(sd1, aw1[l], tp.h[l]);
       }
       pin2(sa0, sd0);
       pin2(sa1, sd1);
@@ -391,7 +416,7 @@ struct ModInv1Level {
         if ((r + 1) % JWV_MOD1_FENCE == 0)
           asm volatile("" : "+v"(vv[r].x), "+v"(vv[r].y) :: "memory");
     }
-    lds_barrier();
+    JWV_MOD_BAR();
     if constexpr (j == J0) {
       const bool dfast = t0 + T <= N && (((uintptr_t)(dst + t0)) & 15) == 0;
 #pragma unroll
@@ -444,7 +469,7 @@ struct ModInv1Level {
           // st = 1: output 2(s0+m)+q, tap l -> double 2m + q + l of the run;
           // st >= 2: slot m + l of the run, half q
           const double x = st == 1 ? v[2 * m + q + l] : v[2 * (m + l) + q];
-          s = mac<FMA>(s, x, ISW ? tp.h[l] : tp.g[l]);
+          s = mod_mac<FMA>(s, x, ISW ? tp.h[l] : tp.g[l]);
         }
         acc[m][q] = s;
       }
@@ -484,7 +509,7 @@ struct ModInv1Level {
       }
       asm volatile("" ::: "memory");  // slot fence
     }
-    lds_barrier();
+    JWV_MOD_BAR();
     // final level, whole tile inside the signal, 16-B aligned output: buffer stores
     const bool dfast = j == J0 && t0 + T <= N && (((uintptr_t)(dst + t0)) & 15) == 0;
 #pragma unroll

@@ -235,6 +235,18 @@ def test_wpt_config4_shape(ctx, ctx_fma):
     assert_close(T.wpt_reverse(yr, w, 6, ctx_fma), xr_ref, "wpt cfg4 rev fma")
 
 
+@pytest.mark.parametrize("B", [3, 64, 97])
+def test_wpt_batch_runs(ctx, B):
+    """Batches whose rows the streamed kernels share out in runs of tiles
+    that start and end inside rows: every row exact."""
+    w = jw.by_class("Symlet8")
+    x = np.stack([rnd(1 << 16, 900 + i) for i in range(B)])
+    yr = oracle.batch("wpt", True, w, x, 6)
+    assert_exact(T.wpt_forward(x, w, 6, ctx), yr, "wpt batch %d fwd" % B)
+    assert_exact(T.wpt_reverse(yr, w, 6, ctx), oracle.batch("wpt", False, w, yr, 6),
+                 "wpt batch %d rev" % B)
+
+
 def test_wpt_config4_full_batch(ctx, ctx_fma):
     """Config 4 at its full shape in ONE call per direction: 4096 Symlet8
     signals x 65536, 6 levels (WaveletPacketTransform.java:73-191 per signal),
@@ -437,6 +449,17 @@ def test_modwt_config5_full_size(ctx, ctx_fma):
     assert_close(cf, cr, "modwt fma")
     d = float(np.abs(T.modwt_inverse(cf, w, ctx_fma) - oracle.modwt_inverse(w, cr)).max())
     assert d <= RT_GATE, "config 5 FMA round trip vs oracle round trip: %g" % d
+
+
+@pytest.mark.parametrize("n", [1_000_003, 2_097_152, 3_333_331])
+def test_modwt_chunked_sizes(ctx, n):
+    """J = 8 signals of many 512-sample tiles: inverse chunks of several tiles,
+    chunk ends inside and at the end of the signal (wrap), ragged last tile."""
+    w = jw.by_class("Daubechies4")
+    x = rnd(n, 5)
+    cr = oracle.modwt_forward(w, x, 8)
+    assert_exact(T.modwt_forward(x, w, 8, ctx), cr, "modwt n=%d" % n)
+    assert_exact(T.modwt_inverse(cr, w, ctx), oracle.modwt_inverse(w, cr), "imodwt n=%d" % n)
 
 
 def test_modwt_direct_vs_sparse_oracle():
