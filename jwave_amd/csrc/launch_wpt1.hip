@@ -102,10 +102,9 @@ hipError_t wfs_k(const Bank& b, const TileArgs& a, hipStream_t s) {
   const int64_t ntile = a.nouter * (a.h / T);
   int64_t nb = (int64_t)per * cu_count();
   if (nb > ntile) nb = ntile;
-  FwdTaps<L> tp;
-  for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
-  hipLaunchKernelGGL(k, dim3((unsigned)nb), dim3(NT), lds, s, a.src, a.sv, a.dst, a.dv, a.h, ntile,
-                     tp);
+  WptStreamArgs<FwdTaps<L>> args{a.src, a.sv, a.dst, a.dv, ntile, a.h, 0, {}};
+  for (int j = 0; j < L; ++j) { args.tp.lo[j] = b.lo[j]; args.tp.hi[j] = b.hi[j]; }
+  hipLaunchKernelGGL(k, dim3((unsigned)nb), dim3(NT), lds, s, args);
   return hipGetLastError();
 }
 template <int L>
@@ -146,10 +145,9 @@ hipError_t wrs_k(const Bank& b, const TileArgs& a, hipStream_t s) {
   const int64_t ntile = a.nouter * (a.h / T);
   int64_t nb = (int64_t)per * cu_count();
   if (nb > ntile) nb = ntile;
-  RevTaps<L> tp;
-  for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
-  hipLaunchKernelGGL(k, dim3((unsigned)nb), dim3(NT), lds, s, a.src, a.sv, a.dst, a.dv, a.h, ntile,
-                     tp);
+  WptStreamArgs<RevTaps<L>> args{a.src, a.sv, a.dst, a.dv, ntile, a.h, 0, {}};
+  for (int j = 0; j < L; ++j) { args.tp.lo_r[j] = b.lo_r[j]; args.tp.hi_r[j] = b.hi_r[j]; }
+  hipLaunchKernelGGL(k, dim3((unsigned)nb), dim3(NT), lds, s, args);
   return hipGetLastError();
 }
 template <int L>

@@ -18,9 +18,42 @@
 // rightmost tile takes its carries from a prologue that runs the halo
 // recursion once (at most one per row per block).
 #pragma once
+#include <cstddef>
 #include "wpt1_kernels.hpp"
 
 namespace jwv {
+
+// The streamed kernels' single argument.  Their tile loop keeps more scalar
+// state live than the one-tile kernels, and with the 32 FP64 taps (64 SGPRs)
+// held across it the compiler spilled SGPRs to VGPR lanes (one v_readlane
+// per tap use in the reverse: 2.6 readlanes per FP64 instruction).  So every
+// level reloads the taps from the kernel-argument segment (scalar loads,
+// K$ hits) and they live only inside the level.
+template <typename Taps>
+struct WptStreamArgs {
+  const double* src;
+  AxisView sv;
+  double* dst;
+  AxisView dv;
+  int64_t ntile;
+  int h;
+  int pad_;
+  Taps tp;
+};
+template <typename Taps>
+__device__ __forceinline__ Taps stream_taps() {
+  using CD = const __attribute__((address_space(4))) double;
+  constexpr int n = sizeof(Taps) / sizeof(double);
+  static_assert(offsetof(WptStreamArgs<Taps>, tp) % 8 == 0, "taps at a double boundary");
+  CD* p = (CD*)((const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr() +
+                offsetof(WptStreamArgs<Taps>, tp));
+  asm volatile("" : "+s"(p));  // a fresh pointer per level: loads stay in the level
+  Taps t;
+  double* d = reinterpret_cast<double*>(&t);
+#pragma unroll
+  for (int i = 0; i < n; ++i) d[i] = p[i];
+  return t;
+}
 
 template <int L, int T, int K>
 struct WptFStreamGeo {
@@ -89,8 +122,9 @@ struct WptFStream {
   // Level l turns np(l) packets of E(l-1) samples into 2 np(l) packets of
   // E(l); the first Q0 of every output packet are the carry of level l.
   template <int l>
-  __device__ __forceinline__ static void pro_level(const FwdTaps<L>& tp, double* lds) {
+  __device__ __forceinline__ static void pro_level(double* lds) {
     if constexpr (l < K) {
+      const FwdTaps<L> tp = stream_taps<FwdTaps<L>>();
       constexpr int mi = G::E(l - 1), mo = G::E(l), npk = G::np(l);
       constexpr int NPR = npk * mo, R = (NPR + NT - 1) / NT;  // pairs
       const int tid = opaque_tid();
@@ -123,20 +157,20 @@ struct WptFStream {
         }
       }
       lds_barrier();
-      pro_level<l + 1>(tp, lds);
+      pro_level<l + 1>(lds);
     }
   }
 
   // ---- main loop: level l of tile t of the row at y
   template <int l>
-  __device__ __forceinline__ static void level(const FwdTaps<L>& tp, double* lds,
-                                               double* __restrict__ y, int h, int t,
+  __device__ __forceinline__ static void level(double* lds, double* __restrict__ y, int h, int t,
                                                const double* __restrict__ rown, int sn,
                                                double2 (&rx)[kQX]) {
     constexpr int mi = G::m(l), Tli = G::Tl(l);
     constexpr int NC = T / 4, R = NC / NT, CPP = Tli / 4;  // couples, per lane, per packet
     static_assert(R * NT == NC, "T = 4 NT R");
     const int tid = opaque_tid();
+    const FwdTaps<L> tp = stream_taps<FwdTaps<L>>();
     const double* in = lds + G::buf(l & 1);
     // carry traffic in registers (read before the sums, written after):
     // the tails of this level's output packets (heads of tile t+1's) and the
@@ -215,7 +249,7 @@ struct WptFStream {
       fetch<G::m(1)>(rx, rown, sn, h);
     }
     lds_barrier();
-    if constexpr (l < K) level<l + 1>(tp, lds, y, h, t, rown, sn, rx);
+    if constexpr (l < K) level<l + 1>(lds, y, h, t, rown, sn, rx);
   }
 };
 
@@ -223,10 +257,13 @@ struct WptFStream {
 // tile) in contiguous runs; a block walks its run from the top.  src / dst
 // rows as in wpt_fwd_tile1 (16-B aligned rows, h a multiple of T).
 template <int L, int NT, int T, int K, bool FMA>
-__global__ __launch_bounds__(NT) void wpt_fwd_stream(const double* __restrict__ src, AxisView sv,
-                                                     double* __restrict__ dst, AxisView dv, int h,
-                                                     int64_t ntile, FwdTaps<L> tp) {
+__global__ __launch_bounds__(NT) void wpt_fwd_stream(WptStreamArgs<FwdTaps<L>> args) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
+  const double* __restrict__ src = args.src;
+  double* __restrict__ dst = args.dst;
+  const AxisView sv = args.sv, dv = args.dv;
+  const int h = args.h;
+  const int64_t ntile = args.ntile;
   using S = WptFStream<L, NT, T, K, FMA>;
   using G = WptFStreamGeo<L, T, K>;
   const int64_t b = blockIdx.x, nb = gridDim.x;
@@ -256,10 +293,10 @@ __global__ __launch_bounds__(NT) void wpt_fwd_stream(const double* __restrict__ 
       S::template fetch<G::E(0)>(px, src + view_base(sv, o), c1, h);
       S::template put<G::E(0)>(lds + G::preg(0), px);
       lds_barrier();
-      S::template pro_level<1>(tp, lds);
+      S::template pro_level<1>(lds);
     }
     const int64_t gn = next_of(next_of(g)), on = gn / ntr;
-    S::template level<1>(tp, lds, dst + view_base(dv, o), h, t, src + view_base(sv, on),
+    S::template level<1>(lds, dst + view_base(dv, o), h, t, src + view_base(sv, on),
                          (int)(gn - on * ntr) * T, rx);
   }
 }
@@ -347,8 +384,9 @@ struct WptRStream {
   // D(l) + 1 for l = K: the band load; else 2 P(l+1)), and writes np(l-1)
   // packets of 2 P(l) values; every level-l data tail (H) is a carry.
   template <int l>
-  __device__ __forceinline__ static void pro_level(const RevTaps<L>& tp, double* lds, double* pb) {
+  __device__ __forceinline__ static void pro_level(double* lds, double* pb) {
     if constexpr (l >= 2) {
+      const RevTaps<L> tp = stream_taps<RevTaps<L>>();
       constexpr int si = l == K ? G::D(K) : 2 * G::P(l + 1);  // input packet stride
       constexpr int bi = si - G::D(l);                          // first used value
       constexpr int pl = G::P(l), so = 2 * pl, nw = G::np(l - 1);
@@ -387,20 +425,20 @@ struct WptRStream {
         for (int v = tid; v < G::np(1) * H; v += NT) c1[v] = out[(v / H) * so + so - H + v % H];
         lds_barrier();
       }
-      pro_level<l - 1>(tp, lds, pb);
+      pro_level<l - 1>(lds, pb);
     }
   }
 
   // ---- main loop: level l of tile t (row output y)
   template <int l>
-  __device__ __forceinline__ static void level(const RevTaps<L>& tp, double* lds,
-                                               double* __restrict__ y, int t, bool head,
+  __device__ __forceinline__ static void level(double* lds, double* __restrict__ y, int t, bool head,
                                                const double* __restrict__ rown, int tn, int h,
                                                double2 (&rb)[kQB]) {
     constexpr int mi = G::m(l), Tli = G::Tl(l);
     constexpr int NC = T / 4, R = NC / NT, NCW = Tli / 2;  // couples, per lane, per packet
     static_assert(R * NT == NC, "T = 4 NT R");
     const int tid = opaque_tid();
+    const RevTaps<L> tp = stream_taps<RevTaps<L>>();
     const double* in = lds + G::buf(l & 1);
     // carries in registers: the halo of level-(l-1) data (l >= 2) and the
     // tails of this level's input packets (l < K) for the next tile
@@ -490,7 +528,7 @@ struct WptRStream {
       fetch(rb, rown, tn, h);
     }
     lds_barrier();
-    if constexpr (l > 1) level<l - 1>(tp, lds, y, t, head, rown, tn, h, rb);
+    if constexpr (l > 1) level<l - 1>(lds, y, t, head, rown, tn, h, rb);
   }
 };
 
@@ -498,10 +536,13 @@ struct WptRStream {
 // contiguous runs, walked upwards.  src: rows of 2^K bands (packets of h/2^K),
 // dst: rows of h samples (16-B aligned rows, h a multiple of T).
 template <int L, int NT, int T, int K, bool FMA>
-__global__ __launch_bounds__(NT) void wpt_rev_stream(const double* __restrict__ src, AxisView sv,
-                                                     double* __restrict__ dst, AxisView dv, int h,
-                                                     int64_t ntile, RevTaps<L> tp) {
+__global__ __launch_bounds__(NT) void wpt_rev_stream(WptStreamArgs<RevTaps<L>> args) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
+  const double* __restrict__ src = args.src;
+  double* __restrict__ dst = args.dst;
+  const AxisView sv = args.sv, dv = args.dv;
+  const int h = args.h;
+  const int64_t ntile = args.ntile;
   using S = WptRStream<L, NT, T, K, FMA>;
   using G = WptRStreamGeo<L, T, K>;
   const int64_t b = blockIdx.x, nb = gridDim.x;
@@ -537,10 +578,10 @@ __global__ __launch_bounds__(NT) void wpt_rev_stream(const double* __restrict__ 
         pin[v] = row[(int64_t)p * hp + x];
       }
       lds_barrier();
-      S::template pro_level<K>(tp, lds, pb);
+      S::template pro_level<K>(lds, pb);
     }
     const int64_t gn = next_of(next_of(g)), on = gn / ntr;
-    S::template level<K>(tp, lds, dst + view_base(dv, o), t, t == 0, src + view_base(sv, on),
+    S::template level<K>(lds, dst + view_base(dv, o), t, t == 0, src + view_base(sv, on),
                          (int)(gn - on * ntr), h, rb);
   }
 }
