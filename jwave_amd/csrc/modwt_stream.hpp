@@ -391,11 +391,10 @@ struct ModFStreamGeo {
     return (b + 1) & ~1;
   }
   static constexpr int buf(int p) { return p ? bsize(0) : 0; }
-  static constexpr int carry0() { return bsize(0) + bsize(1); }
-  static constexpr int lds_doubles() { return carry0() + ncarry(); }
   // prologue: V_j on [c0 - D(j), c0), D(J1-1) = C(J1), D(j) = D(j+1) + C(j+1);
   // x on [c0 - D(0) - pad, c0).  Regions: Q(odd j) at 0, Q(even j) after it,
-  // X at the end (it may overlap the carries and Q(even): dead after level 1)
+  // both below the carries (which the prologue writes level by level); X at
+  // the end, over the carries (it is read only before level 1's barrier)
   static constexpr int D(int j) {
     int d = 0;
     for (int i = j + 1; i <= J1; ++i) d += C(i);
@@ -403,10 +402,13 @@ struct ModFStreamGeo {
   }
   static constexpr int XP() { return D(0) + (D(0) & 1); }  // padded x extent (even)
   static constexpr int q(int p) { return p ? ((D(1) + 3) & ~1) : 0; }
+  static constexpr int qend() { return (q(1) + D(2) + 3) & ~1; }
+  static constexpr int carry0() {
+    return bsize(0) + bsize(1) > qend() ? bsize(0) + bsize(1) : qend();
+  }
+  static constexpr int lds_doubles() { return carry0() + ncarry(); }
   static constexpr int qx() { return lds_doubles() - ((XP() + 3) & ~1); }
-  static_assert(q(0) + D(1) + 2 <= q(1) && q(1) + D(2) + 2 <= lds_doubles() && qx() >= q(1),
-                "prologue regions fit");
-  static_assert(qx() >= q(1) + 0 && qx() >= ((D(1) + 3) & ~1), "x window clear of Q(odd)");
+  static_assert(q(0) + D(1) + 2 <= q(1) && qend() <= carry0() && qx() >= 0, "prologue regions");
   static_assert(T % 2 == 0 && (J1 & 1) == 0 && C(J1) <= T, "geometry");
 };
 
