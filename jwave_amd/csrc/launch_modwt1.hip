@@ -7,7 +7,6 @@
 #include "modwt_stream.hpp"
 #include "jwv_modwt1.hpp"
 
-#include <cstdlib>
 
 #ifndef JWV_FMA
 #error "JWV_FMA must be 0 or 1"
@@ -63,17 +62,6 @@ hipError_t inv_kp(const Bank& b, const ModwtArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// Streamed inverse (modwt_stream.hpp): chunks of 512-output tiles walked
-// right to left with carried halos, one chunk per resident block.  Needs
-// 16-B aligned W rows (ldw even) and V_J input.  env JWV_MODWT_STREAM=1 (A/B
-// this round).
-int stream_env() {
-  static const int v = [] {
-    const char* e = std::getenv("JWV_MODWT_STREAM");
-    return e ? std::atoi(e) : 0;
-  }();
-  return v;
-}
 int cu_count() {
   static const int v = [] {
     int dev = 0, n = 0;
@@ -84,49 +72,12 @@ int cu_count() {
   }();
   return v;
 }
-template <int L, int J1, int kSNT, int kST>
-bool inv_stream_g(const Bank& b, const ModwtArgs& a, hipStream_t s, hipError_t& err) {
-  if constexpr ((J1 & 1) != 0) {
-    return false;
-  } else {
-    // 16-B pieces that never straddle the wrap (N, ldw even; aligned rows),
-    // windows shorter than the signal (wrap at most once), 32-bit offsets
-    using G = ModStreamGeo<L, kST, J1>;
-    if (!stream_env() || (a.N & 1) || (a.ldw & 1) ||
-        (((uintptr_t)a.coef | (uintptr_t)a.src | (uintptr_t)a.vout) & 15) ||
-        a.N < 2 * (G::E(J1) + G::Wn(J1)) || a.N * 8 >= (int64_t(1) << 31))
-      return false;
-    auto k = modwt_inv_stream<L, kSNT, kST, J1, kFMA>;
-    const size_t lds = (size_t)ModStreamGeo<L, kST, J1>::lds_doubles() * sizeof(double);
-    if ((err = prep(k, lds))) return true;
-    int per = 0;
-    if ((err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, kSNT, lds))) return true;
-    if (per < 1) per = 1;
-    const int64_t ntile = (a.N + kST - 1) / kST;
-    int64_t nb = (int64_t)per * cu_count();
-    if (nb > ntile) nb = ntile;
-    hipLaunchKernelGGL(k, dim3((unsigned)nb), dim3(kSNT), lds, s, a.src, a.coef, a.ldw, a.vout,
-                       a.N, ntile, taps<L>(b));
-    err = hipGetLastError();
-    return true;
-  }
-}
-template <int L, int J1>
-bool inv_stream(const Bank& b, const ModwtArgs& a, hipStream_t s, hipError_t& err) {
-  if (stream_env() == 2) return inv_stream_g<L, J1, 512, 1024>(b, a, s, err);
-  return inv_stream_g<L, J1, 256, 512>(b, a, s, err);
-}
-
 // Streamed forward (modwt_stream.hpp): chunks of 1024-sample tiles walked
-// left to right with carried halos.  env JWV_MODWT_FSTREAM=1 (256 threads,
-// two pairs per lane) or 2 (512 threads) (A/B this round).
-int fstream_env() {
-  static const int v = [] {
-    const char* e = std::getenv("JWV_MODWT_FSTREAM");
-    return e ? std::atoi(e) : 0;
-  }();
-  return v;
-}
+// left to right with carried halos, one chunk per resident block (512
+// threads, 3 blocks per CU).  Config 5 forward 172-175 -> 164-165 us
+// (r04e/r04f, one box each, two rounds; 256 x 1024: 173-175, 1024 x 2048:
+// 188, 512 x 2048: 172-173).  Needs N and ldw even and 16-B aligned rows;
+// else the tile kernel.
 template <int L, int J1, int NT, int T>
 bool fwd_stream_g(const Bank& b, const ModwtArgs& a, hipStream_t s, hipError_t& err) {
   if constexpr ((J1 & 1) != 0) {
@@ -154,10 +105,7 @@ bool fwd_stream_g(const Bank& b, const ModwtArgs& a, hipStream_t s, hipError_t& 
 }
 template <int L, int J1>
 bool fwd_stream(const Bank& b, const ModwtArgs& a, hipStream_t s, hipError_t& err) {
-  const int v = fstream_env();
-  if (v == 1) return fwd_stream_g<L, J1, 256, 1024>(b, a, s, err);
-  if (v == 2) return fwd_stream_g<L, J1, 512, 1024>(b, a, s, err);
-  return false;
+  return fwd_stream_g<L, J1, 512, 1024>(b, a, s, err);
 }
 
 template <int L, int J1>
@@ -171,11 +119,7 @@ hipError_t fwd_k(const Bank& b, const ModwtArgs& a, hipStream_t s) {
 }
 template <int L, int J1>
 hipError_t inv_k(const Bank& b, const ModwtArgs& a, hipStream_t s) {
-  if constexpr (J1 == 8) {
-    hipError_t e = hipSuccess;
-    if (inv_stream<L, J1>(b, a, s, e)) return e;
-    return inv_kp<L, J1, 303>(b, a, s);
-  }
+  if constexpr (J1 == 8) return inv_kp<L, J1, 303>(b, a, s);
   return inv_kp<L, J1, 1>(b, a, s);
 }
 template <int L, bool FWD>

@@ -1,9 +1,6 @@
 // launch_wpt1.hip — dispatch of the C = 1 compile-time-geometry WPT tiles
 // (wpt1_kernels.hpp) for one math mode (compiled twice).
 #include "wpt1_kernels.hpp"
-#include "wpt_stream.hpp"
-
-#include <cstdlib>
 #include "jwv_launch.hpp"
 
 #ifndef JWV_FMA
@@ -69,108 +66,8 @@ hipError_t wpt8k_fwd(const Bank& b, const TileArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k, grid, dim3(512), lds, s, a.src, a.sv, a.dst, a.dv, a.h, tp);
   return hipGetLastError();
 }
-// Streamed forward (wpt_stream.hpp): runs of tiles per resident block with
-// carried halos.  env JWV_WPT_FSTREAM=1 (256 x 2048), 2 (512 x 2048),
-// 3 (256 x 4096) (A/B this round).
-int wfstream_env() {
-  static const int v = [] {
-    const char* e = std::getenv("JWV_WPT_FSTREAM");
-    return e ? std::atoi(e) : 0;
-  }();
-  return v;
-}
-int cu_count() {
-  static const int v = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1)
-      n = 256;
-    return n;
-  }();
-  return v;
-}
-template <int L, int NT, int T>
-hipError_t wfs_k(const Bank& b, const TileArgs& a, hipStream_t s) {
-  constexpr int K = 6;
-  using G = WptFStreamGeo<L, T, K>;
-  auto k = wpt_fwd_stream<L, NT, T, K, kFMA>;
-  const size_t lds = (size_t)G::lds_doubles() * sizeof(double);
-  if (hipError_t e = prep1(k, lds)) return e;
-  int per = 0;
-  if (hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, NT, lds)) return e;
-  if (per < 1) per = 1;
-  const int64_t ntile = a.nouter * (a.h / T);
-  int64_t nb = (int64_t)per * cu_count();
-  if (nb > ntile) nb = ntile;
-  WptStreamArgs<FwdTaps<L>> args{a.src, a.sv, a.dst, a.dv, ntile, a.h, 0, {}};
-  for (int j = 0; j < L; ++j) { args.tp.lo[j] = b.lo[j]; args.tp.hi[j] = b.hi[j]; }
-  hipLaunchKernelGGL(k, dim3((unsigned)nb), dim3(NT), lds, s, args);
-  return hipGetLastError();
-}
-template <int L>
-bool wpt_fstream(const Bank& b, const TileArgs& a, hipStream_t s, hipError_t& err) {
-  if constexpr (L != 16) {
-    return false;
-  } else {
-    const int v = wfstream_env();
-    // contiguous rows of whole packets (pk == 1), 6 levels, rows fit int offsets
-    if (!v || a.K != 6 || a.sv.pk != 1 || a.dv.pk != 1 || a.h % 4096 || a.h < 8192 ||
-        (int64_t)a.h * 8 >= (int64_t(1) << 31))
-      return false;
-    if (v == 1) err = wfs_k<L, 256, 2048>(b, a, s);
-    else if (v == 2) err = wfs_k<L, 512, 2048>(b, a, s);
-    else err = wfs_k<L, 256, 4096>(b, a, s);
-    return true;
-  }
-}
-// Streamed reverse (wpt_stream.hpp).  env JWV_WPT_RSTREAM=1 (256 x 2048),
-// 2 (512 x 2048), 3 (256 x 4096) (A/B this round).
-int wrstream_env() {
-  static const int v = [] {
-    const char* e = std::getenv("JWV_WPT_RSTREAM");
-    return e ? std::atoi(e) : 0;
-  }();
-  return v;
-}
-template <int L, int NT, int T>
-hipError_t wrs_k(const Bank& b, const TileArgs& a, hipStream_t s) {
-  constexpr int K = 6;
-  using G = WptRStreamGeo<L, T, K>;
-  auto k = wpt_rev_stream<L, NT, T, K, kFMA>;
-  const size_t lds = (size_t)G::lds_doubles() * sizeof(double);
-  if (hipError_t e = prep1(k, lds)) return e;
-  int per = 0;
-  if (hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, NT, lds)) return e;
-  if (per < 1) per = 1;
-  const int64_t ntile = a.nouter * (a.h / T);
-  int64_t nb = (int64_t)per * cu_count();
-  if (nb > ntile) nb = ntile;
-  WptStreamArgs<RevTaps<L>> args{a.src, a.sv, a.dst, a.dv, ntile, a.h, 0, {}};
-  for (int j = 0; j < L; ++j) { args.tp.lo_r[j] = b.lo_r[j]; args.tp.hi_r[j] = b.hi_r[j]; }
-  hipLaunchKernelGGL(k, dim3((unsigned)nb), dim3(NT), lds, s, args);
-  return hipGetLastError();
-}
-template <int L>
-bool wpt_rstream(const Bank& b, const TileArgs& a, hipStream_t s, hipError_t& err) {
-  if constexpr (L != 16) {
-    return false;
-  } else {
-    const int v = wrstream_env();
-    if (!v || a.K != 6 || a.sv.pk != 1 || a.dv.pk != 1 || a.h % 4096 || a.h < 8192 ||
-        (int64_t)a.h * 8 >= (int64_t(1) << 31))
-      return false;
-    if (v == 1) err = wrs_k<L, 256, 2048>(b, a, s);
-    else if (v == 2) err = wrs_k<L, 512, 2048>(b, a, s);
-    else err = wrs_k<L, 256, 4096>(b, a, s);
-    return true;
-  }
-}
 template <int L>
 hipError_t wpt1_l(const Bank& b, const TileArgs& a, hipStream_t s, bool fwd) {
-  {
-    hipError_t e = hipSuccess;
-    if (fwd ? wpt_fstream<L>(b, a, s, e) : wpt_rstream<L>(b, a, s, e)) return e;
-  }
   if (fwd && a.K == 6 && a.h % 8192 == 0) return wpt8k_fwd<L>(b, a, s);
   switch (a.K) {
     case 1: return fwd ? wfwd1_k<L, 1>(b, a, s) : wrev1_k<L, 1>(b, a, s);

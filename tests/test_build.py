@@ -31,8 +31,6 @@ def test_library_reads_no_variant_switches():
     from jwave_amd import _lib
     blob = open(_lib.LIB_PATH, "rb").read()
     names = set(re.findall(rb"JWV_[A-Z0-9_]+", blob))
-    allowed = {b"JWV_LAUNCH", b"JWV_LAUNCH_LOG", b"JWV_TRANSFORM_FWT", b"JWV_TRANSFORM_WPT",
-               b"JWV_MODWT_STREAM", b"JWV_MODWT_FSTREAM",
-               b"JWV_WPT_FSTREAM", b"JWV_WPT_RSTREAM"}  # A/B this round
+    allowed = {b"JWV_LAUNCH", b"JWV_LAUNCH_LOG", b"JWV_TRANSFORM_FWT", b"JWV_TRANSFORM_WPT"}
     assert names <= allowed, sorted(names - allowed)
     assert b"JWV_WPT_DIAGW" not in blob
