@@ -1200,11 +1200,15 @@ hipError_t launch_fwt_fwd_res(const Bank& b, bool fma, int C, const ResArgs& a, 
   hipError_t e = hipSuccess;
   if (C == 1 && (fma ? fused::fwt_fwd_res1(b, a, s, e) : exact::fwt_fwd_res1(b, a, s, e)))
     return e;
+  if (C == 8 && (fma ? fused::fwt_res16(b, a, s, true, e) : exact::fwt_res16(b, a, s, true, e)))
+    return e;
   JWV_MODE2(fwt_fwd_res, b, C, a, s);
 }
 hipError_t launch_fwt_rev_res(const Bank& b, bool fma, int C, const ResArgs& a, hipStream_t s) {
   hipError_t e = hipSuccess;
   if (C == 1 && (fma ? fused::fwt_rev_res1(b, a, s, e) : exact::fwt_rev_res1(b, a, s, e)))
+    return e;
+  if (C == 8 && (fma ? fused::fwt_res16(b, a, s, false, e) : exact::fwt_res16(b, a, s, false, e)))
     return e;
   JWV_MODE2(fwt_rev_res, b, C, a, s);
 }

@@ -188,6 +188,7 @@ bool fwt_rev_res1(const Bank&, const ResArgs&, hipStream_t, hipError_t& err);
 bool fwt_fwd_tile1(const Bank&, const TileArgs&, hipStream_t, hipError_t& err);
 bool fwt_rev_tile1(const Bank&, const TileArgs&, hipStream_t, hipError_t& err);
 bool fwt_tile8(const Bank&, const TileArgs&, hipStream_t, bool fwd, hipError_t& err);
+bool fwt_res16(const Bank&, const ResArgs&, hipStream_t, bool fwd, hipError_t& err);
 hipError_t fwt_fwd_res(const Bank&, int C, const ResArgs&, hipStream_t);
 hipError_t fwt_rev_res(const Bank&, int C, const ResArgs&, hipStream_t);
 hipError_t fwt_fwd_tile(const Bank&, int C, const TileArgs&, hipStream_t);
@@ -211,6 +212,7 @@ bool fwt_rev_res1(const Bank&, const ResArgs&, hipStream_t, hipError_t& err);
 bool fwt_fwd_tile1(const Bank&, const TileArgs&, hipStream_t, hipError_t& err);
 bool fwt_rev_tile1(const Bank&, const TileArgs&, hipStream_t, hipError_t& err);
 bool fwt_tile8(const Bank&, const TileArgs&, hipStream_t, bool fwd, hipError_t& err);
+bool fwt_res16(const Bank&, const ResArgs&, hipStream_t, bool fwd, hipError_t& err);
 hipError_t fwt_fwd_res(const Bank&, int C, const ResArgs&, hipStream_t);
 hipError_t fwt_rev_res(const Bank&, int C, const ResArgs&, hipStream_t);
 hipError_t fwt_fwd_tile(const Bank&, int C, const TileArgs&, hipStream_t);

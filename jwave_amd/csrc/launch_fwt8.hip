@@ -1,6 +1,7 @@
 // launch_fwt8.hip — dispatch of the C = 8 column-slab tiles
 // (fwt8_kernels.hpp) for one math mode (compiled twice).
 #include "fwt16_kernels.hpp"
+#include "fwt1_row.hpp"
 #include "jwv_launch.hpp"
 
 #ifndef JWV_FMA
@@ -102,9 +103,50 @@ hipError_t tile8_l(const Bank& b, const TileArgs& a, hipStream_t s, bool fwd) {
   }
 }
 
+template <int L, int CW>
+hipError_t res16_cw(const Bank& b, const ResArgs& a, hipStream_t s) {
+  const int htop = a.n << (a.nlev - 1);
+  const size_t lds = (size_t)CW * col16_stride(htop) * sizeof(double);
+  const dim3 grid((unsigned)(a.nouter * (a.inner / CW)));
+  auto k = fwt_rev_col16<L, kFMA, CW>;
+  if (hipError_t e = prep1(k, lds)) return e;
+  RevTaps<L> tp;
+  for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
+  hipLaunchKernelGGL(k, grid, dim3(64 * CW), lds, s, a.src, a.sv, a.dst, a.dv, a.n, a.nlev,
+                     a.inner, tp);
+  return hipGetLastError();
+}
+template <int L>
+hipError_t res16_l(const Bank& b, const ResArgs& a, hipStream_t s, bool fwd) {
+  // the half-slab pairing is a bijection for whole groups of 16 blocks
+  const bool half = (a.nouter * (a.inner / 8)) % 16 == 0;
+  return half ? res16_cw<L, 8>(b, a, s) : res16_cw<L, 16>(b, a, s);
+}
 }  // namespace
 
 namespace JWV_NS {
+// Reverse resident tails of column passes with one wave per column
+// (fwt1_row.hpp): XCD-paired half slabs, 16-B aligned row segments, a
+// compiled-in tap count, at most kSmallH rows.  Config 3 reverse column tail
+// 74-75 -> 60-61 us (r04h: 16-column blocks 69 us); the forward keeps the
+// block-per-slab kernel (70 us against 73 / 90 us for 16 / 8 columns).
+bool fwt_res16(const Bank& b, const ResArgs& a, hipStream_t s, bool fwd, hipError_t& err) {
+  if (fwd) return false;
+  if (!a.dma || a.inner % kColW || a.nlev < 1 || a.sv.pk != 1 || a.dv.pk != 1) return false;
+  if (!fwd && b.scale != 1.0) return false;
+  if ((a.sv.s_len & 1) || (a.dv.s_len & 1) || (a.sv.s_outer & 1) || (a.dv.s_outer & 1) ||
+      (((uintptr_t)a.src | (uintptr_t)a.dst) & 15))
+    return false;
+  const int64_t htop = fwd ? a.n : ((int64_t)a.n << (a.nlev - 1));
+  if (htop > kSmallH || htop < 2) return false;
+  switch (b.L) {
+    case 2: err = res16_l<2>(b, a, s, fwd); return true;
+    case 4: err = res16_l<4>(b, a, s, fwd); return true;
+    case 8: err = res16_l<8>(b, a, s, fwd); return true;
+    case 16: err = res16_l<16>(b, a, s, fwd); return true;
+    default: return false;
+  }
+}
 // C = 8 slabs: every row segment 16-B aligned (a.dma), whole slabs, a
 // compiled-in tap count, at most Geo::kFwtK8 levels (the generic bound).
 bool fwt_tile8(const Bank& b, const TileArgs& a, hipStream_t s, bool fwd, hipError_t& err) {
