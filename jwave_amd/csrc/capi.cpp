@@ -37,6 +37,10 @@ using jwv::AxisView;
 using jwv::Bank;
 using jwv::Geo;
 
+namespace jwv {
+thread_local LaunchEvents g_launch_ev;  // jwv_launch.hpp
+}
+
 namespace {
 
 thread_local std::string g_tls_error;
@@ -289,12 +293,22 @@ struct ProfScope {
     if (log) std::fprintf(stderr, "JWV_LAUNCH %s %.0f\n", kKindNames[kind], bytes);
     if (!on) return;
     jwv_ctx::Rec r{kind, bytes, take_event(c), take_event(c)};
-    hipchk(hipEventRecord(r.e0, c->stream), "hipEventRecord");
     c->recs.push_back(r);
     idx = c->recs.size() - 1;
+    // the scope's first JWV_LAUNCH records both events in its dispatch packet
+    jwv::g_launch_ev = {r.e0, r.e1, 0};
   }
   ~ProfScope() {
-    if (on) hipEventRecord(c->recs[idx].e1, c->stream);
+    if (!on) return;
+    const int n = jwv::g_launch_ev.launches;
+    jwv::g_launch_ev = {};
+    const jwv_ctx::Rec& r = c->recs[idx];
+    if (n == 0) {  // nothing launched (a copy): an empty span
+      hipEventRecord(r.e0, c->stream);
+      hipEventRecord(r.e1, c->stream);
+    } else if (n > 1) {  // several launches: first start to last end
+      hipEventRecord(r.e1, c->stream);
+    }
   }
 };
 

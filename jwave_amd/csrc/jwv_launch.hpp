@@ -2,11 +2,32 @@
 // (capi.cpp) and the kernel translation units (launch_*.hip).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 
 #include "jwv_device.hpp"
 
 namespace jwv {
+
+// Kernel timing for the planner's profiled pass (capi.cpp ProfScope): while
+// a scope is open, the first kernel launched through JWV_LAUNCH carries the
+// scope's start / stop events in its own dispatch packet
+// (hipExtLaunchKernelGGL), so the elapsed time is the kernel's execution
+// alone, as rocprofv3 reports it (events recorded as separate commands
+// around the launch added ~6 us per launch of queue latency).
+struct LaunchEvents {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int launches = 0;
+};
+extern thread_local LaunchEvents g_launch_ev;
+#define JWV_LAUNCH(kernel, grid, block, lds, stream, ...)                                      \
+  do {                                                                                        \
+    if (::jwv::g_launch_ev.e0 && ::jwv::g_launch_ev.launches++ == 0)                          \
+      hipExtLaunchKernelGGL(kernel, grid, block, lds, stream, ::jwv::g_launch_ev.e0,           \
+                            ::jwv::g_launch_ev.e1, 0, __VA_ARGS__);                           \
+    else                                                                                      \
+      hipLaunchKernelGGL(kernel, grid, block, lds, stream, __VA_ARGS__);                     \
+  } while (0)
 
 // Host copy of a filter bank (Wavelet getters, Wavelet.java:152-219).
 struct Bank {

@@ -37,7 +37,7 @@ hipError_t fwd_l(const Bank& b, const ChainFwdArgs& a, hipStream_t s) {
   if (hipError_t e = prep_c(k, lds)) return e;
   FwdTaps<L> tp;
   for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
-  hipLaunchKernelGGL(k, dim3((unsigned)(a.h / CG::kTAf)), dim3(NT), lds, s, a.src, a.dst, a.wsA,
+  JWV_LAUNCH(k, dim3((unsigned)(a.h / CG::kTAf)), dim3(NT), lds, s, a.src, a.dst, a.wsA,
                      a.wsB, a.cnt, a.h, a.levC, tp);
   return hipGetLastError();
 }
@@ -63,7 +63,7 @@ hipError_t rev_l(const Bank& b, const ChainRevArgs& a, hipStream_t s) {
   if (G < 1 + nM) return hipErrorLaunchOutOfResources;  // M roles must all be co-resident
   RevTaps<L> tp;
   for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
-  hipLaunchKernelGGL(k, dim3((unsigned)G), dim3(NT), lds, s, a.coef, a.dst, a.wsR, a.wsM, a.ctl,
+  JWV_LAUNCH(k, dim3((unsigned)G), dim3(NT), lds, s, a.coef, a.dst, a.wsR, a.wsM, a.ctl,
                      a.h, a.h0R, a.nR, a.epoch, a.spins, tp);
   return hipGetLastError();
 }
@@ -81,7 +81,7 @@ hipError_t head_l(const Bank& b, const RevHeadArgs& a, hipStream_t s) {
   if (hipError_t e = prep_c(k, lds)) return e;
   RevTaps<L> tp;
   for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
-  hipLaunchKernelGGL(k, dim3((unsigned)nM), dim3(NTH), lds, s, a.coef, a.wsM, a.h0R, a.nR, tp);
+  JWV_LAUNCH(k, dim3((unsigned)nM), dim3(NTH), lds, s, a.coef, a.wsM, a.h0R, a.nR, tp);
   return hipGetLastError();
 }
 }  // namespace

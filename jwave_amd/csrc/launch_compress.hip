@@ -163,16 +163,16 @@ hipError_t launch_compress_magnitude(const double* c, double* y, int64_t n, doub
   const int np = compress_partials(n);
   double* out = scratch + np;
   const unsigned g = grid_of(n);
-  hipLaunchKernelGGL(abs_sum_partial, dim3(np), dim3(kRB), 0, s, c, n, scratch);
-  hipLaunchKernelGGL(abs_sum_final, dim3(1), dim3(kRB), 0, s, scratch, np, n, threshold, out);
+  JWV_LAUNCH(abs_sum_partial, dim3(np), dim3(kRB), 0, s, c, n, scratch);
+  JWV_LAUNCH(abs_sum_final, dim3(1), dim3(kRB), 0, s, scratch, np, n, threshold, out);
   if (c != y) {
-    hipLaunchKernelGGL(apply_cut<0>, dim3(g), dim3(256), 0, s, c, y, n, out);
-    hipLaunchKernelGGL(abs_sum_serial, dim3(1), dim3(64), 0, s, c, n, threshold, out);
-    hipLaunchKernelGGL(apply_cut<3>, dim3(g), dim3(256), 0, s, c, y, n, out);
+    JWV_LAUNCH(apply_cut<0>, dim3(g), dim3(256), 0, s, c, y, n, out);
+    JWV_LAUNCH(abs_sum_serial, dim3(1), dim3(64), 0, s, c, n, threshold, out);
+    JWV_LAUNCH(apply_cut<3>, dim3(g), dim3(256), 0, s, c, y, n, out);
   } else {
-    hipLaunchKernelGGL(apply_cut<1>, dim3(g), dim3(256), 0, s, c, y, n, out);
-    hipLaunchKernelGGL(abs_sum_serial, dim3(1), dim3(64), 0, s, c, n, threshold, out);
-    hipLaunchKernelGGL(apply_cut<2>, dim3(g), dim3(256), 0, s, c, y, n, out);
+    JWV_LAUNCH(apply_cut<1>, dim3(g), dim3(256), 0, s, c, y, n, out);
+    JWV_LAUNCH(abs_sum_serial, dim3(1), dim3(64), 0, s, c, n, threshold, out);
+    JWV_LAUNCH(apply_cut<2>, dim3(g), dim3(256), 0, s, c, y, n, out);
   }
   return hipGetLastError();
 }

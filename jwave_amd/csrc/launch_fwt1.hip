@@ -39,7 +39,7 @@ hipError_t fwd1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
   FwdTaps<L> tp;
   for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
   const dim3 grid((unsigned)(a.nouter * (a.h / T)));
-  hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.sv.s_outer, a.dst, a.dv.s_outer, a.adst,
+  JWV_LAUNCH(k, grid, dim3(NT), lds, s, a.src, a.sv.s_outer, a.dst, a.dv.s_outer, a.adst,
                      a.av.s_outer, a.h, tp, a.sp);
   return hipGetLastError();
 }
@@ -78,7 +78,7 @@ hipError_t rev1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
   for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
   const int hK = a.h << (a.K - 1);
   const dim3 grid((unsigned)(a.nouter * (hK / T)));
-  hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.sv.s_outer, a.coef, a.cv.s_outer, a.dst,
+  JWV_LAUNCH(k, grid, dim3(NT), lds, s, a.src, a.sv.s_outer, a.coef, a.cv.s_outer, a.dst,
                      a.dv.s_outer, hK, tp, a.sp);
   return hipGetLastError();
 }
@@ -111,7 +111,7 @@ hipError_t fwd_res1_l(const Bank& b, const ResArgs& a, hipStream_t s) {
   const dim3 grid((unsigned)a.nouter);
   auto k = fwt_fwd_res1<L, NTX, CAPX, kFMA>;
   if (hipError_t e = prep1(k, lds)) return e;
-  hipLaunchKernelGGL(k, grid, dim3(NTX), lds, s, a.src, a.sv.s_outer, a.dst, a.dv.s_outer, a.n,
+  JWV_LAUNCH(k, grid, dim3(NTX), lds, s, a.src, a.sv.s_outer, a.dst, a.dv.s_outer, a.n,
                      a.nlev, tp);
   return hipGetLastError();
 }
@@ -124,7 +124,7 @@ hipError_t rev_res1_l(const Bank& b, const ResArgs& a, hipStream_t s) {
   const dim3 grid((unsigned)a.nouter);
   auto k = fwt_rev_res1<L, NTX, CAPX, kFMA>;
   if (hipError_t e = prep1(k, lds)) return e;
-  hipLaunchKernelGGL(k, grid, dim3(NTX), lds, s, a.src, a.sv.s_outer, a.dst, a.dv.s_outer, a.n,
+  JWV_LAUNCH(k, grid, dim3(NTX), lds, s, a.src, a.sv.s_outer, a.dst, a.dv.s_outer, a.n,
                      a.nlev, tp);
   return hipGetLastError();
 }
@@ -171,7 +171,7 @@ hipError_t fwd_small1_l(const Bank& b, const ResArgs& a, hipStream_t s) {
   FwdTaps<L> tp;
   for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
   auto k = fwt_fwd_small1<L, kFMA>;
-  hipLaunchKernelGGL(k, dim3((unsigned)((a.nouter + kSmallRows - 1) / kSmallRows)),
+  JWV_LAUNCH(k, dim3((unsigned)((a.nouter + kSmallRows - 1) / kSmallRows)),
                      dim3(64 * kSmallRows), 0, s, a.src, a.sv.s_outer, a.dst, a.dv.s_outer, a.n,
                      a.nlev, a.nouter, tp);
   return hipGetLastError();
@@ -181,7 +181,7 @@ hipError_t rev_small1_l(const Bank& b, const ResArgs& a, hipStream_t s) {
   RevTaps<L> tp;
   for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
   auto k = fwt_rev_small1<L, kFMA>;
-  hipLaunchKernelGGL(k, dim3((unsigned)((a.nouter + kSmallRows - 1) / kSmallRows)),
+  JWV_LAUNCH(k, dim3((unsigned)((a.nouter + kSmallRows - 1) / kSmallRows)),
                      dim3(64 * kSmallRows), 0, s, a.src, a.sv.s_outer, a.dst, a.dv.s_outer, a.n,
                      a.nlev, a.nouter, tp);
   return hipGetLastError();

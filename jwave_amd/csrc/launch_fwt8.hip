@@ -35,7 +35,7 @@ hipError_t fwd8_k(const Bank& b, const TileArgs& a, hipStream_t s) {
   FwdTaps<L> tp;
   for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
   const dim3 grid((unsigned)(a.nouter * (a.inner / 8) * (a.h / kT8)));
-  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a.src, a.sv, a.dst, a.dv, a.adst, a.av, a.h,
+  JWV_LAUNCH(k, grid, dim3(256), lds, s, a.src, a.sv, a.dst, a.dv, a.adst, a.av, a.h,
                      a.inner, tp, Geo::slab_order());
   return hipGetLastError();
 }
@@ -48,7 +48,7 @@ hipError_t rev8_k(const Bank& b, const TileArgs& a, hipStream_t s) {
   for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
   const int hK = a.h << (a.K - 1);
   const dim3 grid((unsigned)(a.nouter * (a.inner / 8) * (hK / kT8)));
-  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a.src, a.sv, a.coef, a.cv, a.dst, a.dv, hK,
+  JWV_LAUNCH(k, grid, dim3(256), lds, s, a.src, a.sv, a.coef, a.cv, a.dst, a.dv, hK,
                      a.inner, tp, Geo::slab_order());
   return hipGetLastError();
 }
@@ -65,7 +65,7 @@ hipError_t fwd16_k(const Bank& b, const TileArgs& a, hipStream_t s) {
   FwdTaps<L> tp;
   for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
   const dim3 grid((unsigned)(a.nouter * (a.inner / 16) * (a.h / kT16F)));
-  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a.src, a.sv, a.dst, a.dv, a.adst, a.av, a.h,
+  JWV_LAUNCH(k, grid, dim3(256), lds, s, a.src, a.sv, a.dst, a.dv, a.adst, a.av, a.h,
                      a.inner, tp, Geo::slab_order());
   return hipGetLastError();
 }
@@ -78,7 +78,7 @@ hipError_t rev16_k(const Bank& b, const TileArgs& a, hipStream_t s) {
   for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
   const int hK = a.h << (a.K - 1);
   const dim3 grid((unsigned)(a.nouter * (a.inner / 16) * (hK / kT16R)));
-  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a.src, a.sv, a.coef, a.cv, a.dst, a.dv, hK,
+  JWV_LAUNCH(k, grid, dim3(256), lds, s, a.src, a.sv, a.coef, a.cv, a.dst, a.dv, hK,
                      a.inner, tp, Geo::slab_order());
   return hipGetLastError();
 }
@@ -112,7 +112,7 @@ hipError_t res16_cw(const Bank& b, const ResArgs& a, hipStream_t s) {
   if (hipError_t e = prep1(k, lds)) return e;
   RevTaps<L> tp;
   for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
-  hipLaunchKernelGGL(k, grid, dim3(64 * CW), lds, s, a.src, a.sv, a.dst, a.dv, a.n, a.nlev,
+  JWV_LAUNCH(k, grid, dim3(64 * CW), lds, s, a.src, a.sv, a.dst, a.dv, a.n, a.nlev,
                      a.inner, tp);
   return hipGetLastError();
 }

@@ -82,7 +82,7 @@ hipError_t fwt_fwd_res_nt(const Bank& b, const ResArgs& a, hipStream_t s) {
   const size_t lds = (size_t)(a.n + 2) * C * sizeof(double);
   if (hipError_t e = prep(k, lds)) return e;
   const dim3 grid((unsigned)(a.nouter * ncb(a.inner, C)));
-  hipLaunchKernelGGL(k, grid, dim3(NTX), lds, s, a.src, a.sv, a.dst, a.dv, a.n, a.nlev, a.inner,
+  JWV_LAUNCH(k, grid, dim3(NTX), lds, s, a.src, a.sv, a.dst, a.dv, a.n, a.nlev, a.inner,
                      a.dma, fwd_taps<L>(b));
   return hipGetLastError();
 }
@@ -101,7 +101,7 @@ hipError_t fwt_rev_res_nt(const Bank& b, const ResArgs& a, hipStream_t s) {
   const size_t lds = (size_t)(htop + 2) * C * sizeof(double);
   if (hipError_t e = prep(k, lds)) return e;
   const dim3 grid((unsigned)(a.nouter * ncb(a.inner, C)));
-  hipLaunchKernelGGL(k, grid, dim3(NTX), lds, s, a.src, a.sv, a.dst, a.dv, a.n, a.nlev, a.inner,
+  JWV_LAUNCH(k, grid, dim3(NTX), lds, s, a.src, a.sv, a.dst, a.dv, a.n, a.nlev, a.inner,
                      a.dma, rev_taps<L>(b));
   return hipGetLastError();
 }
@@ -122,7 +122,7 @@ hipError_t fwt_fwd_tile_t(const Bank& b, const TileArgs& a, hipStream_t s) {
   const size_t lds = (size_t)(m0 + 2) * C * sizeof(double);
   if (hipError_t e = prep(k, lds)) return e;
   const dim3 grid((unsigned)(a.nouter * ncb(a.inner, C) * (a.h / T)));
-  hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.sv, a.dst, a.dv, a.adst, a.av, a.h, a.K,
+  JWV_LAUNCH(k, grid, dim3(NT), lds, s, a.src, a.sv, a.dst, a.dv, a.adst, a.av, a.h, a.K,
                      a.inner, a.dma, fwd_taps<L>(b));
   return hipGetLastError();
 }
@@ -141,7 +141,7 @@ hipError_t fwt_rev_tile_t(const Bank& b, const TileArgs& a, hipStream_t s) {
   if (hipError_t e = prep(k, lds)) return e;
   const int hK = a.h << (a.K - 1);
   const dim3 grid((unsigned)(a.nouter * ncb(a.inner, C) * (hK / T)));
-  hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.sv, a.coef, a.cv, a.dst, a.dv, a.h, a.K,
+  JWV_LAUNCH(k, grid, dim3(NT), lds, s, a.src, a.sv, a.coef, a.cv, a.dst, a.dv, a.h, a.K,
                      a.inner, a.dma, rev_taps<L>(b));
   return hipGetLastError();
 }
@@ -157,7 +157,7 @@ hipError_t wpt_fwd_res_go(const Bank& b, const ResArgs& a, hipStream_t s) {
   const size_t lds = (size_t)(a.n + 2) * C * sizeof(double);
   if (hipError_t e = prep(k, lds)) return e;
   const dim3 grid((unsigned)(a.nouter * ncb(a.inner, C)));
-  hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.sv, a.dst, a.dv, a.n, a.nlev, a.inner,
+  JWV_LAUNCH(k, grid, dim3(NT), lds, s, a.src, a.sv, a.dst, a.dv, a.n, a.nlev, a.inner,
                      a.dma, fwd_taps<L>(b));
   return hipGetLastError();
 }
@@ -167,7 +167,7 @@ hipError_t wpt_rev_res_go(const Bank& b, const ResArgs& a, hipStream_t s) {
   const size_t lds = (size_t)(a.n + 2) * C * sizeof(double);
   if (hipError_t e = prep(k, lds)) return e;
   const dim3 grid((unsigned)(a.nouter * ncb(a.inner, C)));
-  hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.sv, a.dst, a.dv, a.n, a.h0, a.nlev,
+  JWV_LAUNCH(k, grid, dim3(NT), lds, s, a.src, a.sv, a.dst, a.dv, a.n, a.h0, a.nlev,
                      a.inner, a.dma, rev_taps<L>(b));
   return hipGetLastError();
 }
@@ -179,7 +179,7 @@ hipError_t wpt_fwd_tile_go(const Bank& b, const TileArgs& a, hipStream_t s) {
   const size_t lds = (size_t)(m0 + 2) * C * sizeof(double);
   if (hipError_t e = prep(k, lds)) return e;
   const dim3 grid((unsigned)(a.nouter * ncb(a.inner, C) * (a.h / T)));
-  hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.sv, a.dst, a.dv, a.h, a.K, a.inner,
+  JWV_LAUNCH(k, grid, dim3(NT), lds, s, a.src, a.sv, a.dst, a.dv, a.h, a.K, a.inner,
                      a.dma, fwd_taps<L>(b));
   return hipGetLastError();
 }
@@ -191,7 +191,7 @@ hipError_t wpt_rev_tile_go(const Bank& b, const TileArgs& a, hipStream_t s) {
   const size_t lds = (size_t)(T + (1 << KM) * (2 * QM + 4)) * C * sizeof(double);
   if (hipError_t e = prep(k, lds)) return e;
   const dim3 grid((unsigned)(a.nouter * ncb(a.inner, C) * (a.h / T)));
-  hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.sv, a.dst, a.dv, a.h, a.K, a.inner,
+  JWV_LAUNCH(k, grid, dim3(NT), lds, s, a.src, a.sv, a.dst, a.dv, a.h, a.K, a.inner,
                      a.dma, rev_taps<L>(b));
   return hipGetLastError();
 }
@@ -208,7 +208,7 @@ hipError_t res_var_go(const Bank& b, const VarArgs& a, hipStream_t s) {
   if (hipError_t e = prep(k, lds)) return e;
   TP tp;
   if constexpr (fwd) tp = fwd_taps<L>(b); else tp = rev_taps<L>(b);
-  hipLaunchKernelGGL(k, dim3((unsigned)a.seg.count), dim3(NT), lds, s, a.src, a.dst, a.seg, tp);
+  JWV_LAUNCH(k, dim3((unsigned)a.seg.count), dim3(NT), lds, s, a.src, a.dst, a.seg, tp);
   return hipGetLastError();
 }
 template <int OP>

@@ -57,7 +57,7 @@ hipError_t fwd_tile_go(const Bank& b, const ModwtArgs& a, hipStream_t s) {
   const size_t lds = (size_t)(TX + S) * sizeof(double);
   if (hipError_t e = prep(k, lds)) return e;
   const dim3 grid((unsigned)((a.N + TX - 1) / TX));
-  hipLaunchKernelGGL(k, grid, dim3(NTX), lds, s, a.src, a.wout, a.ldw, a.vout, a.N, a.j0, a.j1,
+  JWV_LAUNCH(k, grid, dim3(NTX), lds, s, a.src, a.wout, a.ldw, a.vout, a.N, a.j0, a.j1,
                      tp);
   return hipGetLastError();
 }
@@ -69,7 +69,7 @@ hipError_t fwd_go(const Bank& b, bool tiled, const ModwtArgs& a, hipStream_t s) 
   }
   const auto tp = mtaps<L>(b);
   auto k = modwt_fwd_level<L, kFMA>;
-  hipLaunchKernelGGL(k, dim3(level_grid(a.N)), dim3(256), 0, s, a.src,
+  JWV_LAUNCH(k, dim3(level_grid(a.N)), dim3(256), 0, s, a.src,
                      a.wout + (int64_t)(a.j0 - 1) * a.ldw, a.vout, a.N, a.j0, tp);
   return hipGetLastError();
 }
@@ -82,7 +82,7 @@ hipError_t inv_tile_go(const Bank& b, const ModwtArgs& a, hipStream_t s) {
   const size_t lds = (size_t)2 * (TX + R) * sizeof(double);
   if (hipError_t e = prep(k, lds)) return e;
   const dim3 grid((unsigned)((a.N + TX - 1) / TX));
-  hipLaunchKernelGGL(k, grid, dim3(NTX), lds, s, a.src, a.coef, a.ldw, a.vout, a.N, a.j0, a.j1,
+  JWV_LAUNCH(k, grid, dim3(NTX), lds, s, a.src, a.coef, a.ldw, a.vout, a.N, a.j0, a.j1,
                      tp);
   return hipGetLastError();
 }
@@ -98,7 +98,7 @@ hipError_t inv_tile_cm_go(const Bank& b, const ModwtArgs& a, hipStream_t s) {
     const size_t lds = (size_t)2 * buf * sizeof(double);
     if (hipError_t e = prep(k, lds)) return e;
     const dim3 grid((unsigned)((a.N + TX - 1) / TX));
-    hipLaunchKernelGGL(k, grid, dim3(NTX), lds, s, a.src, a.coef, a.ldw, a.vout, a.N, a.j0,
+    JWV_LAUNCH(k, grid, dim3(NTX), lds, s, a.src, a.coef, a.ldw, a.vout, a.N, a.j0,
                        a.j1, buf, tp);
     return hipGetLastError();
   }
@@ -111,7 +111,7 @@ hipError_t inv_go(const Bank& b, bool tiled, const ModwtArgs& a, hipStream_t s) 
   }
   const auto tp = mtaps<L>(b);
   auto k = modwt_inv_level<L, kFMA>;
-  hipLaunchKernelGGL(k, dim3(level_grid(a.N)), dim3(256), 0, s, a.src,
+  JWV_LAUNCH(k, dim3(level_grid(a.N)), dim3(256), 0, s, a.src,
                      a.coef + (int64_t)(a.j0 - 1) * a.ldw, a.vout, a.N, a.j0, tp);
   return hipGetLastError();
 }
@@ -162,7 +162,7 @@ hipError_t launch_copy_axis(const double* src, AxisView sv, double* dst, AxisVie
   if (total == 0) return hipSuccess;
   int64_t g = (total + 255) / 256;
   if (g > 16384) g = 16384;
-  hipLaunchKernelGGL(copy_axis_kernel, dim3((unsigned)g), dim3(256), 0, s, src, sv, dst, dv,
+  JWV_LAUNCH(copy_axis_kernel, dim3((unsigned)g), dim3(256), 0, s, src, sv, dst, dv,
                      nouter, len, inner);
   return hipGetLastError();
 }

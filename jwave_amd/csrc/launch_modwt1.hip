@@ -49,7 +49,7 @@ hipError_t fwd_kp(const Bank& b, const ModwtArgs& a, hipStream_t s) {
   const size_t lds = (size_t)ModFwd1Geo<L, TF, 1, J1>::lds_doubles(1) * sizeof(double);
   if (hipError_t e = prep(k, lds)) return e;
   const dim3 grid((unsigned)((a.N + TF - 1) / TF));
-  hipLaunchKernelGGL(k, grid, dim3(NT), lds, s, a.src, a.wout, a.ldw, a.vout, a.N, taps<L>(b));
+  JWV_LAUNCH(k, grid, dim3(NT), lds, s, a.src, a.wout, a.ldw, a.vout, a.N, taps<L>(b));
   return hipGetLastError();
 }
 template <int L, int J1, int M>
@@ -58,7 +58,7 @@ hipError_t inv_kp(const Bank& b, const ModwtArgs& a, hipStream_t s) {
   const size_t lds = (size_t)ModInv1Geo<L, kTI, 1, J1>::lds_doubles(M) * sizeof(double);
   if (hipError_t e = prep(k, lds)) return e;
   const dim3 grid((unsigned)((a.N + kTI - 1) / kTI));
-  hipLaunchKernelGGL(k, grid, dim3(kNT), lds, s, a.src, a.coef, a.ldw, a.vout, a.N, taps<L>(b));
+  JWV_LAUNCH(k, grid, dim3(kNT), lds, s, a.src, a.coef, a.ldw, a.vout, a.N, taps<L>(b));
   return hipGetLastError();
 }
 
@@ -97,7 +97,7 @@ bool fwd_stream_g(const Bank& b, const ModwtArgs& a, hipStream_t s, hipError_t& 
     const int64_t ntile = (a.N + T - 1) / T;
     int64_t nb = (int64_t)per * cu_count();
     if (nb > ntile) nb = ntile;
-    hipLaunchKernelGGL(k, dim3((unsigned)nb), dim3(NT), lds, s, a.src, a.wout, a.ldw, a.vout,
+    JWV_LAUNCH(k, dim3((unsigned)nb), dim3(NT), lds, s, a.src, a.wout, a.ldw, a.vout,
                        a.N, ntile, taps<L>(b));
     err = hipGetLastError();
     return true;

@@ -31,7 +31,7 @@ hipError_t tail_k(const Bank& b, const TailArgs& a, hipStream_t s) {
       return e;
   FwdTaps<L> tp;
   for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
-  hipLaunchKernelGGL(k, dim3((unsigned)(a.hB / kTailTB)), dim3(NT), lds, s, a.src, a.dst, a.wsB,
+  JWV_LAUNCH(k, dim3((unsigned)(a.hB / kTailTB)), dim3(NT), lds, s, a.src, a.dst, a.wsB,
                      a.cnt, a.hB, a.levC, tp);
   return hipGetLastError();
 }

@@ -33,7 +33,7 @@ hipError_t wfwd1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
   FwdTaps<L> tp;
   for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
   const dim3 grid((unsigned)(a.nouter * (a.h / kWptT)));
-  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a.src, a.sv, a.dst, a.dv, a.h, tp);
+  JWV_LAUNCH(k, grid, dim3(256), lds, s, a.src, a.sv, a.dst, a.dv, a.h, tp);
   return hipGetLastError();
 }
 // The reverse tiles' couples as four interleaved sums (rev_couple_ilv) for
@@ -47,7 +47,7 @@ hipError_t wrev1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
   RevTaps<L> tp;
   for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
   const dim3 grid((unsigned)(a.nouter * (a.h / kWptT)));
-  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a.src, a.sv, a.dst, a.dv, a.h, tp);
+  JWV_LAUNCH(k, grid, dim3(256), lds, s, a.src, a.sv, a.dst, a.dv, a.h, tp);
   return hipGetLastError();
 }
 // 8192-sample forward WPT tiles, 512 threads: half the halo recompute of the
@@ -63,7 +63,7 @@ hipError_t wpt8k_fwd(const Bank& b, const TileArgs& a, hipStream_t s) {
   if (hipError_t e = prep1(k, lds)) return e;
   FwdTaps<L> tp;
   for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
-  hipLaunchKernelGGL(k, grid, dim3(512), lds, s, a.src, a.sv, a.dst, a.dv, a.h, tp);
+  JWV_LAUNCH(k, grid, dim3(512), lds, s, a.src, a.sv, a.dst, a.dv, a.h, tp);
   return hipGetLastError();
 }
 template <int L>
