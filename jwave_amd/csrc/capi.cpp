@@ -57,7 +57,7 @@ struct DevBuf {
 // on the way out), so the PCIe transfer runs at the pinned rate instead of
 // the driver's pageable path.  Pinned caller memory (hipHostMalloc /
 // jwv_host_alloc / hipHostRegister) is DMA'd directly.
-constexpr size_t kPinChunk = size_t(8) << 20;  // bytes per slot
+constexpr size_t kPinChunk = size_t(32) << 20;  // bytes per slot
 constexpr int kPinSlots = 4;
 
 // A few host threads for the pageable <-> pinned copies (one core's memcpy
