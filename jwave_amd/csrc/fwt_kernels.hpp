@@ -370,13 +370,27 @@ __device__ __forceinline__ void fwt_fwd_res_blk(const double* __restrict__ s, Ax
   JWV_STAMP(42);
 }
 
+// Slab of block b for the resident column passes: with 8-column slabs the
+// two halves of every 128-B row line belong to slabs 2k and 2k+1; blocks b
+// and b + 8 share an XCD (round-robin dealing) and start together, so they
+// take a slab pair and the line is fetched from HBM once (bijective for
+// grids of whole 16-block groups; otherwise the plain order).
+template <int C>
+__device__ __forceinline__ int64_t res_slab_block(int64_t b) {
+  if constexpr (C == 8) {
+    if ((gridDim.x & 15) == 0) return ((b >> 4) * 8 + (b & 7)) * 2 + ((b >> 3) & 1);
+  }
+  return b;
+}
+
 template <int L, int C, int NT, int CAP, bool FMA>
 __global__ __launch_bounds__(NT) void fwt_fwd_res(const double* __restrict__ src, AxisView sv,
     double* __restrict__ dst, AxisView dv, int h0, int nlev, int inner, int dma,
     typename FB<L>::Fwd tp) {
   const int ncb = (inner + C - 1) / C;
-  const int64_t o = blockIdx.x / ncb;
-  const int c0 = (blockIdx.x % ncb) * C;
+  const int64_t bs = res_slab_block<C>(blockIdx.x);
+  const int64_t o = bs / ncb;
+  const int c0 = (int)(bs % ncb) * C;
   const double* s = src + view_base(sv, o) + c0;
   double* y = dst + view_base(dv, o) + c0;
   fwt_fwd_res_blk<L, C, NT, CAP, FMA>(s, sv, y, dv, h0, nlev, c0, inner, dma, tp);
@@ -610,8 +624,9 @@ __global__ __launch_bounds__(NT) void fwt_rev_res(const double* __restrict__ src
     double* __restrict__ dst, AxisView dv, int h0, int nlev, int inner, int dma,
     typename FB<L>::Rev tp) {
   const int ncb = (inner + C - 1) / C;
-  const int64_t o = blockIdx.x / ncb;
-  const int c0 = (blockIdx.x % ncb) * C;
+  const int64_t bs = res_slab_block<C>(blockIdx.x);
+  const int64_t o = bs / ncb;
+  const int c0 = (int)(bs % ncb) * C;
   const double* s = src + view_base(sv, o) + c0;
   double* y = dst + view_base(dv, o) + c0;
   fwt_rev_res_blk<L, C, NT, CAP, FMA>(s, sv, y, dv, h0, nlev, c0, inner, dma, tp);
