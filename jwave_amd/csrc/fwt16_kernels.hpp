@@ -162,13 +162,15 @@ __global__ __launch_bounds__(NT) void fwt_fwd_tile16(const double* __restrict__ 
 }
 
 // ---------------------------------------------------------------- reverse
-template <int L, int T, int K>
+template <int L, int T, int K, bool IP>
 struct Rev16Geo {
   using G = Rev1Geo<L, T, K>;
-  static constexpr int lds_doubles() { return 16 * G::lds_doubles(); }
+  static constexpr int lds_doubles() { return 16 * (IP ? G::ip_lds_doubles() : G::lds_doubles()); }
 };
 
-template <int L, int NT, int T, int K, bool FMA, int l>
+// IP: Rev1Geo's in-place layout (rows of 16); a level's outputs wait in
+// registers until every lane has read its inputs (second barrier).
+template <int L, int NT, int T, int K, bool FMA, int l, bool IP>
 struct Rev16Level {
   __device__ __forceinline__ static void run(const RevTaps<L>& tp, double* lds, int t,
                                              double* __restrict__ y, int64_t sl) {
@@ -181,9 +183,11 @@ struct Rev16Level {
     // head pairs (global pair index < Q-1) exist only in the first tiles, and
     // there only in slot 0: ml < Q-1 + c(l)/2
     static_assert(16 * (Q - 1 + G::c(l) / 2) <= NT, "head pairs must sit in slot 0");
-    const double* ab = lds + 16 * ((((l + 1) & 1) != 0) ? G::buf1() : G::buf0());
-    const double* db = lds + 16 * G::doff(l);
-    double* ob = lds + 16 * (((l & 1) != 0) ? G::buf1() : G::buf0());
+    const double* ab = lds + 16 * (IP ? 0 : (((l + 1) & 1) != 0) ? G::buf1() : G::buf0());
+    const double* db = lds + 16 * (IP ? G::ip_doff(l) : G::doff(l));
+    double* ob = lds + 16 * (IP ? 0 : ((l & 1) != 0) ? G::buf1() : G::buf0());
+    constexpr bool DEF = IP && l > 0;
+    double2 dres[DEF ? R : 1];
     const int tid = opaque_tid();  // per-level: keeps address math out of the prologue
     const int pbase = t * (T >> (l + 1)) - G::c(l) / 2;  // global index of window pair 0
 #pragma unroll
@@ -207,15 +211,31 @@ struct Rev16Level {
           double* yo = y + ((int64_t)t * T + 2 * ml) * sl + c;
           yo[0] = xe;
           yo[sl] = xo;
+        } else if constexpr (DEF) {
+          // slot fence: the next slot's window reads stay below this one
+          asm volatile("" : "+v"(xe), "+v"(xo)::"memory");
+          dres[r] = make_double2(xe, xo);
         } else {
           ob[(2 * ml) * 16 + c] = xe;
           ob[(2 * ml + 1) * 16 + c] = xo;
         }
       }
     }
+    if constexpr (DEF) {
+      lds_barrier();
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int w = tid + r * NT;
+        if ((r + 1) * NT <= NI || w < NI) {
+          const int c = w & 15, ml = w >> 4;
+          ob[(2 * ml) * 16 + c] = dres[r].x;
+          ob[(2 * ml + 1) * 16 + c] = dres[r].y;
+        }
+      }
+    }
     if constexpr (l > 0) {
       lds_barrier();
-      Rev16Level<L, NT, T, K, FMA, l - 1>::run(tp, lds, t, y, sl);
+      Rev16Level<L, NT, T, K, FMA, l - 1, IP>::run(tp, lds, t, y, sl);
     }
   }
 };
@@ -223,7 +243,7 @@ struct Rev16Level {
 // Grid: nouter * (inner/16) * (hK/T) blocks.  asrc: level-K approximation
 // (view as, length hK >> K); coef: coefficient array (view cv, details of
 // level size h at rows [h/2, h)); dst: output rows [0, hK) (view dv).
-template <int L, int NT, int T, int K, bool FMA>
+template <int L, int NT, int T, int K, bool FMA, bool IP>
 __global__ __launch_bounds__(NT) void fwt_rev_tile16(const double* __restrict__ asrc, AxisView as,
                                                      const double* __restrict__ coef, AxisView cv,
                                                      double* __restrict__ dst, AxisView dv, int hK,
@@ -246,19 +266,21 @@ __global__ __launch_bounds__(NT) void fwt_rev_tile16(const double* __restrict__ 
   {
     const int BK = (t * T >> K) - G::c(K);
     const int am = (hK >> K) - 1;
-    load_window<16, NT, 1>(lds + 16 * ((K & 1) ? G::buf1() : G::buf0()), sa, G::len(K), true, 0,
+    load_window<16, NT, 1>(lds + 16 * (IP ? 0 : (K & 1) ? G::buf1() : G::buf0()), sa, G::len(K),
+                           true, 0,
                            inner, [&](int e) { return (int64_t)((BK + e) & am) * asl; });
   }
 #pragma unroll
   for (int l = K - 1; l >= 0; --l) {
     const int half = hK >> (l + 1), hm = half - 1;
     const int B = (t * T >> (l + 1)) - G::c(l + 1);
-    load_window<16, NT, 1>(lds + 16 * G::doff(l), sc, G::len(l + 1), true, 0, inner, [&](int e) {
+    load_window<16, NT, 1>(lds + 16 * (IP ? G::ip_doff(l) : G::doff(l)), sc, G::len(l + 1), true,
+                           0, inner, [&](int e) {
       return ((int64_t)half + ((B + e) & hm)) * csl;
     });
   }
   dma_fence_barrier();
-  Rev16Level<L, NT, T, K, FMA, K - 1>::run(tp, lds, t, dst + view_base(dv, o) + c0, dv.s_len);
+  Rev16Level<L, NT, T, K, FMA, K - 1, IP>::run(tp, lds, t, dst + view_base(dv, o) + c0, dv.s_len);
 }
 
 }  // namespace jwv

@@ -169,7 +169,24 @@ struct Rev1Geo {
   static constexpr int lds_doubles() {
     return dtotal() + len(1) + (K >= 2 ? (len(2) > len(K) ? len(2) : len(K)) : 0) + 4;
   }
+  // In-place layout (IP): [a_K | d_{K-1} | ... | d_0].  Every level reads its
+  // approximations at 0 and writes its outputs over [0, len(l)) once every
+  // lane has read (a second barrier per level), so LDS holds the input
+  // windows only: rows of config 3 (T = 2048, K = 3) 27 -> 17 KB, 16-column
+  // slabs (T = 256) 61 -> 39 KB, i.e. 5 -> 7 and 2 -> 4 blocks per CU.
+  static constexpr int ip_doff(int l) {
+    int o = len(K);
+    for (int k = K - 1; k > l; --k) o += len(k + 1);
+    return o;
+  }
+  static constexpr int ip_lds_doubles() { return ip_doff(-1) + 4; }
+  static constexpr bool ip_fits() {  // level l's outputs end before d_{l-1}
+    for (int l = 1; l < K; ++l)
+      if (len(l) > ip_doff(l - 1)) return false;
+    return true;
+  }
   static_assert(((T >> K) & 1) == 0, "T/2^K must be even");
+  static_assert(ip_fits(), "in-place level outputs must not reach unread windows");
 };
 
 // Each lane synthesises two adjacent pairs (ml, ml+1) of one level ("a
@@ -179,7 +196,8 @@ struct Rev1Geo {
 #ifndef JWV_REV_COUPLE0
 #define JWV_REV_COUPLE0 1
 #endif
-template <int L, int NT, int T, int K, bool FMA, int l, bool WT = false, bool CP = false>
+template <int L, int NT, int T, int K, bool FMA, int l, bool WT = false, bool CP = false,
+          bool IP = false>
 struct Rev1Level {
   __device__ __forceinline__ static void run(const RevTaps<L>& tp, double* lds, int t,
                                              double* __restrict__ y, int sp = 0) {
@@ -204,19 +222,37 @@ struct Rev1Level {
     // lane at level 0).
     constexpr bool kCouple = CP && L >= 12 && (l > 0 || JWV_REV_COUPLE0);
     static_assert(Q - 2 + G::c(l) / 2 < NT, "array-head pairs must sit in slot 0");
-    const double* ab = lds + ((((l + 1) & 1) != 0) ? G::buf1() : G::buf0());
-    const double* db = lds + G::doff(l);
-    double* ob = lds + (((l & 1) != 0) ? G::buf1() : G::buf0());
+    const double* ab = lds + (IP ? 0 : (((l + 1) & 1) != 0) ? G::buf1() : G::buf0());
+    const double* db = lds + (IP ? G::ip_doff(l) : G::doff(l));
+    double* ob = lds + (IP ? 0 : ((l & 1) != 0) ? G::buf1() : G::buf0());
     const int tid = opaque_tid();  // per-level: keeps address math out of the prologue
     const int pbase = t * (T >> (l + 1)) - G::c(l) / 2;  // global index of window pair 0
     auto is_head = [&](int ml) { return pbase + ml >= 0 && pbase + ml < Q - 1; };
-    auto put = [&](int ml, double xe, double xo, bool w) {
-      if (!w) return;
+    auto put_now = [&](int ml, double xe, double xo) {
       if constexpr (l == 0) {  // WT: handed to another workgroup of this launch
         if constexpr (WT) st2<true>(y + (int64_t)t * T + 2 * ml, xe, xo);
         else st2_pol(y + (int64_t)t * T, 2 * ml, xe, xo, sp);
       } else {
         *reinterpret_cast<double2*>(ob + 2 * ml) = make_double2(xe, xo);
+      }
+    };
+    // IP, l > 0: the outputs overwrite this level's inputs, so they wait in
+    // registers (slot i of a compile-time index; ml < 0: nothing to write)
+    // until every lane has read.
+    constexpr bool DEF = IP && l > 0;
+    constexpr int NPUT = DEF ? (kCouple ? 2 * R + 1 : RS) : 1;
+    double2 dres[NPUT];
+    int dml[NPUT];
+#pragma unroll
+    for (int i = 0; i < NPUT; ++i) dml[i] = -1;
+    auto put = [&](int i, int ml, double xe, double xo, bool w) {
+      if constexpr (DEF) {
+        // slot fence: the next slot's window reads stay below this one
+        asm volatile("" : "+v"(xe), "+v"(xo)::"memory");
+        dres[i] = make_double2(xe, xo);
+        dml[i] = w ? ml : -1;
+      } else if (w) {
+        put_now(ml, xe, xo);
       }
     };
     if constexpr (kCouple) {
@@ -250,8 +286,8 @@ struct Rev1Level {
             w0 = !is_head(ml);
             w1 = w1 && !is_head(ml + 1);
           }
-          put(ml, x0e, x0o, w0);
-          put(ml + 1, x1e, x1o, w1);
+          put(2 * r, ml, x0e, x0o, w0);
+          put(2 * r + 1, ml + 1, x1e, x1o, w1);
         }
       }
     } else {
@@ -271,7 +307,7 @@ struct Rev1Level {
           } else {
             rev_pair<L, FMA>(tp, ab + li, db + li, 1, xe, xo);
           }
-          put(ml, xe, xo, true);
+          put(r, ml, xe, xo, true);
         }
       }
     }
@@ -286,12 +322,18 @@ struct Rev1Level {
         double xe, xo;
         rev_pair_rot<L, FMA>(tp, [=](int q) { return ab[li - q]; },
                              [=](int q) { return db[li - q]; }, tid, xe, xo);
-        put(ml, xe, xo, true);
+        put(NPUT - 1, ml, xe, xo, true);
       }
+    }
+    if constexpr (DEF) {
+      lds_barrier();
+#pragma unroll
+      for (int i = 0; i < NPUT; ++i)
+        if (dml[i] >= 0) put_now(dml[i], dres[i].x, dres[i].y);
     }
     if constexpr (l > 0) {
       lds_barrier();
-      Rev1Level<L, NT, T, K, FMA, l - 1, WT, CP>::run(tp, lds, t, y, sp);
+      Rev1Level<L, NT, T, K, FMA, l - 1, WT, CP, IP>::run(tp, lds, t, y, sp);
     }
   }
 };
@@ -299,7 +341,12 @@ struct Rev1Level {
 // Grid: nouter * (hK / T) blocks.  asrc: level-K approximation (length
 // h1/2 = hK >> K); coef: the coefficient array (details of level size h at
 // coef[h/2 ..)); dst: output of length hK.
-template <int L, int NT, int T, int K, bool FMA>
+template <int L, int T, int K, bool IP>
+__host__ __device__ constexpr int rev1_lds_doubles() {
+  return IP ? Rev1Geo<L, T, K>::ip_lds_doubles() : Rev1Geo<L, T, K>::lds_doubles();
+}
+
+template <int L, int NT, int T, int K, bool FMA, bool IP>
 __global__ __launch_bounds__(NT) void fwt_rev_tile1(const double* __restrict__ asrc,
                                                     int64_t s_a, const double* __restrict__ coef,
                                                     int64_t s_c, double* __restrict__ dst,
@@ -318,18 +365,18 @@ __global__ __launch_bounds__(NT) void fwt_rev_tile1(const double* __restrict__ a
   {
     const int BK = (t * T >> K) - G::c(K);
     const int am = (hK >> K) - 1;
-    load_window<1, NT, MAXU>(lds + ((K & 1) ? G::buf1() : G::buf0()), sa, G::len(K), true, 0, 1,
-                             [&](int e) { return (int64_t)((BK + e) & am); });
+    load_window<1, NT, MAXU>(lds + (IP ? 0 : (K & 1) ? G::buf1() : G::buf0()), sa, G::len(K),
+                             true, 0, 1, [&](int e) { return (int64_t)((BK + e) & am); });
   }
 #pragma unroll
   for (int l = K - 1; l >= 0; --l) {
     const int half = hK >> (l + 1), hm = half - 1;
     const int B = (t * T >> (l + 1)) - G::c(l + 1);
-    load_window<1, NT, MAXU>(lds + G::doff(l), sc, G::len(l + 1), true, 0, 1,
-                             [&](int e) { return (int64_t)half + ((B + e) & hm); });
+    load_window<1, NT, MAXU>(lds + (IP ? G::ip_doff(l) : G::doff(l)), sc, G::len(l + 1), true, 0,
+                             1, [&](int e) { return (int64_t)half + ((B + e) & hm); });
   }
   dma_fence_barrier();
-  Rev1Level<L, NT, T, K, FMA, K - 1, false, true>::run(tp, lds, t, dst + o * s_d, sp);
+  Rev1Level<L, NT, T, K, FMA, K - 1, false, true, IP>::run(tp, lds, t, dst + o * s_d, sp);
 }
 
 }  // namespace jwv

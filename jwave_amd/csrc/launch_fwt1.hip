@@ -71,8 +71,9 @@ hipError_t fwd1_l(const Bank& b, const TileArgs& a, hipStream_t s) {
 
 template <int L, int NT, int T, int K>
 hipError_t rev1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
-  auto k = fwt_rev_tile1<L, NT, T, K, kFMA>;
-  const size_t lds = (size_t)Rev1Geo<L, T, K>::lds_doubles() * sizeof(double);
+  constexpr bool IP = true;  // Rev1Geo in-place layout (r04s: rev tiles 269 -> 247 us, config 3)
+  auto k = fwt_rev_tile1<L, NT, T, K, kFMA, IP>;
+  const size_t lds = (size_t)rev1_lds_doubles<L, T, K, IP>() * sizeof(double);
   if (hipError_t e = prep1(k, lds)) return e;
   RevTaps<L> tp;
   for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }

@@ -57,6 +57,7 @@ hipError_t rev8_k(const Bank& b, const TileArgs& a, hipStream_t s) {
 // 256-row tiles (every window in LDS: 61 KB).  Config 3 against the C = 8
 // tiles (r04b, one box, two rounds): 1.368 / 1.371 -> 1.341 / 1.334 ms/step.
 constexpr int kT16F = 512, kT16R = 256;
+constexpr bool kRev16IP = true;  // Rev1Geo in-place layout: 61 -> 39 KB, 2 -> 4 blocks per CU
 template <int L, int K>
 hipError_t fwd16_k(const Bank& b, const TileArgs& a, hipStream_t s) {
   auto k = fwt_fwd_tile16<L, 256, kT16F, K, kFMA>;
@@ -71,8 +72,8 @@ hipError_t fwd16_k(const Bank& b, const TileArgs& a, hipStream_t s) {
 }
 template <int L, int K>
 hipError_t rev16_k(const Bank& b, const TileArgs& a, hipStream_t s) {
-  auto k = fwt_rev_tile16<L, 256, kT16R, K, kFMA>;
-  const size_t lds = (size_t)Rev16Geo<L, kT16R, K>::lds_doubles() * sizeof(double);
+  auto k = fwt_rev_tile16<L, 256, kT16R, K, kFMA, kRev16IP>;
+  const size_t lds = (size_t)Rev16Geo<L, kT16R, K, kRev16IP>::lds_doubles() * sizeof(double);
   if (hipError_t e = prep1(k, lds)) return e;
   RevTaps<L> tp;
   for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
