@@ -15,7 +15,7 @@ if [ "$PART" = a ]; then
   tail -1 $O/bench_fwt1d.json
   timeout -k 10 200 python bench.py --steps 20 --warmup 5 --math fma --no-cpu-baseline > $O/bench_fwt1d_fma.json 2> $O/bench_fwt1d_fma.err || { echo B2 FAILED; exit 3; }
   for wl in fwt2d wpt modwt; do
-    timeout -k 10 300 python bench.py --workload $wl --steps 10 --warmup 3 > $O/bench_$wl.json 2> $O/bench_$wl.err || { echo B3 $wl FAILED; tail $O/bench_$wl.err; exit 4; }
+    timeout -k 10 300 python bench.py --workload $wl --steps 20 --warmup 5 > $O/bench_$wl.json 2> $O/bench_$wl.err || { echo B3 $wl FAILED; tail $O/bench_$wl.err; exit 4; }
     tail -1 $O/bench_$wl.json
   done
   for wl in fwt1d fwt2d wpt modwt; do
