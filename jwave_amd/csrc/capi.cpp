@@ -147,7 +147,8 @@ struct jwv_ctx {
   DevBuf red;    // reduction scratch (CompressorMagnitude)
   DevBuf hin, hout;  // device buffers of the host-pointer entry points
   PinRing pin;       // their pinned host staging (allocated on first use)
-  unsigned tail_calls = 0;  // fused forward tail launches (its counter slot)
+  unsigned tail_base = 0;    // fused forward tail: counter value before the next launch
+  bool tail_dirty = false;   // a tail launch was enqueued by the call in progress
   // single-launch FWT chains: [0, kWords) forward counters, [kWords, 2 kWords)
   // reverse ticket/flags; zeroed once, left zero by every completed launch
   unsigned* sync = nullptr;
@@ -161,6 +162,12 @@ struct jwv_ctx {
   struct Rec { int kind; double bytes; hipEvent_t e0, e1; };
   std::vector<Rec> recs;
   std::vector<hipEvent_t> ev_pool;
+  // overlapped 2-D schedule (body_2d_fwt): side streams for the resident
+  // passes, a ring of ordering events, per-column-group workspace pairs
+  hipStream_t side[2] = {nullptr, nullptr};
+  std::vector<hipEvent_t> xev;
+  size_t xev_next = 0;
+  std::vector<DevBuf> gws;
 };
 
 namespace {
@@ -377,13 +384,13 @@ bool fast1(const Bank& b, const Axis& a, bool rev) {
 // the whole level plan; everything else takes the multi-launch plan below.
 using jwv::ChainGeo;
 
-// [0, kWords) forward chain, [kWords, 2 kWords) reverse chain, then
-// kTailSlots arrival counters of the fused forward tail, one per call in
-// flight (call k uses slot k % kTailSlots; its last arriver re-zeroes it), so
-// tail launches queued on different streams of one context never share a
-// counter.
-constexpr int kTailSlots = 64;
-constexpr size_t kSyncWords = 2 * ChainGeo::kWords + 16 + kTailSlots;
+// [0, kWords) forward chain, [kWords, 2 kWords) reverse chain, then the
+// arrival counter of the fused forward tail (jwv_epoch.hpp: never reset; the
+// context keeps the value it holds between launches in tail_base).  Like the
+// workspace, it belongs to the context's launch stream: a context runs one
+// transform at a time (its mutex), and a launch in flight on one stream must
+// complete before the context is pointed at another (jwave_hip.h).
+constexpr size_t kSyncWords = 2 * ChainGeo::kWords + 16 + 1;
 unsigned* sync_words(jwv_ctx* c) {
   if (!c->sync) {
     HIPCHK(hipMalloc(&c->sync, kSyncWords * sizeof(unsigned)));
@@ -391,44 +398,76 @@ unsigned* sync_words(jwv_ctx* c) {
   }
   return c->sync;
 }
-unsigned* tail_counter(jwv_ctx* c) {
-  unsigned* w = sync_words(c) + 2 * ChainGeo::kWords + 16;
-  return w + (c->tail_calls++ % kTailSlots);
+unsigned* tail_counter(jwv_ctx* c) { return sync_words(c) + 2 * ChainGeo::kWords + 16; }
+// Error path: a failed call may have left a tail launch part-way, so the
+// counter's value is unknown.  Drain the stream and zero the counter and its
+// base together (best effort: if the device is gone the context is too).
+void tail_resync(jwv_ctx* c) {
+  if (!c->sync || !c->tail_dirty) return;
+  c->tail_dirty = false;
+  int prev = -1;
+  if (hipGetDevice(&prev) != hipSuccess || (prev != c->device && hipSetDevice(c->device) != hipSuccess))
+    return;
+  (void)hipStreamSynchronize(c->stream);
+  if (hipMemset(tail_counter(c), 0, sizeof(unsigned)) == hipSuccess) c->tail_base = 0;
+  if (prev != c->device) (void)hipSetDevice(prev);
 }
 
 int plan_of(jwv_ctx* c) { return c->plan >= 0 ? c->plan : ChainGeo::default_plan(); }
 
-bool try_fwd_chain(jwv_ctx* c, const Bank& b, const Axis& a, int nlev) {
-  if (!(plan_of(c) & JWV_PLAN_CHAIN_FWD) || a.outer != 1 || !fast1(b, a, false)) return false;
+// A planned launch of an axis transform.  The planner turns the reference's
+// level loop into steps (tiled passes, the resident pass) before anything is
+// launched, so the overlapped 2-D schedule (body_2d_fwt) can run a plan's
+// resident pass on another stream while tiles of independent columns stream.
+// Every workspace a plan uses is allocated while it is built (grow()
+// synchronises the launch stream, which must not happen between the steps of
+// a schedule that forks other streams).
+struct Step {
+  bool res = false;  // the resident pass (fwt_fwd_res / fwt_rev_res)
+  int h = 0;         // res: forward input length / reverse output length
+  std::function<void()> go;
+};
+using Plan = std::vector<Step>;
+
+void run_plan(const Plan& p) {
+  for (const Step& s : p) s.go();
+}
+
+// One launch per direction (fwt1_chain.hpp) where the compiled geometry covers
+// the plan; an empty function otherwise.
+std::function<void()> fwd_chain_step(jwv_ctx* c, const Bank& b, const Axis& a, int nlev) {
+  if (!(plan_of(c) & JWV_PLAN_CHAIN_FWD) || a.outer != 1 || !fast1(b, a, false)) return {};
   const int64_t h = a.len, hB = h >> ChainGeo::kKA, hC = hB >> ChainGeo::kKB;
   const int64_t mB = ChainGeo::kTB + (int64_t)(b.L - 2) * ((1 << ChainGeo::kKB) - 1);
   const int levC = nlev - ChainGeo::kKA - ChainGeo::kKB;
   if (levC < 0 || h % ChainGeo::kTAf || hB % ChainGeo::kTB || mB > hB || hC > ChainGeo::kCap)
-    return false;
-  if (hB / ChainGeo::kTB + 1 > ChainGeo::kWords) return false;
+    return {};
+  if (hB / ChainGeo::kTB + 1 > ChainGeo::kWords) return {};
   double* wsA = grow(c, c->ws[0], (size_t)hB);
   double* wsB = grow(c, c->ws[1], (size_t)hC);
-  jwv::ChainFwdArgs ca{a.src, a.dst, wsA, wsB, sync_words(c), (int)h, levC};
-  { ProfScope ps_(c, K_FWT_FWD_CHAIN, 16.0 * h);
-    hipchk(jwv::launch_fwt_fwd_chain(b, use_fma(c), ca, c->stream), "fwt_fwd_chain"); }
-  return true;
+  const jwv::ChainFwdArgs ca{a.src, a.dst, wsA, wsB, sync_words(c), (int)h, levC};
+  return [c, &b, ca, h] {
+    ProfScope ps_(c, K_FWT_FWD_CHAIN, 16.0 * h);
+    hipchk(jwv::launch_fwt_fwd_chain(b, use_fma(c), ca, c->stream), "fwt_fwd_chain");
+  };
 }
 
-bool try_rev_chain(jwv_ctx* c, const Bank& b, const Axis& a, int h0) {
-  if (!(plan_of(c) & JWV_PLAN_CHAIN_REV) || a.outer != 1 || !fast1(b, a, true)) return false;
+std::function<void()> rev_chain_step(jwv_ctx* c, const Bank& b, const Axis& a, int h0) {
+  if (!(plan_of(c) & JWV_PLAN_CHAIN_REV) || a.outer != 1 || !fast1(b, a, true)) return {};
   const int64_t h = a.len, hM = h >> ChainGeo::kKAr, hR = hM >> ChainGeo::kKM;
-  if (hM % ChainGeo::kTM || hR < 64 || hR > ChainGeo::kCap || h0 > hR) return false;
-  if (2 + hM / ChainGeo::kTM > ChainGeo::kWords) return false;
+  if (hM % ChainGeo::kTM || hR < 64 || hR > ChainGeo::kCap || h0 > hR) return {};
+  if (2 + hM / ChainGeo::kTM > ChainGeo::kWords) return {};
   const int nR = exponent(hR / h0) + 1;
   double* wsR = grow(c, c->ws[0], (size_t)hR);
   double* wsM = grow(c, c->ws[1], (size_t)hM);
-  if (++c->epoch == 0) c->epoch = 1;
-  jwv::ChainRevArgs ca{a.src, a.dst, wsR, wsM, sync_words(c) + ChainGeo::kWords, (int)h, h0, nR,
-                       c->epoch, c->poll_limit};
-  c->waited = true;
-  { ProfScope ps_(c, K_FWT_REV_CHAIN, 16.0 * h);
-    hipchk(jwv::launch_fwt_rev_chain(b, use_fma(c), ca, c->stream), "fwt_rev_chain"); }
-  return true;
+  return [c, &b, wsR, wsM, a, h, h0, nR] {
+    if (++c->epoch == 0) c->epoch = 1;
+    const jwv::ChainRevArgs ca{a.src, a.dst, wsR, wsM, sync_words(c) + ChainGeo::kWords, (int)h,
+                               h0, nR, c->epoch, c->poll_limit};
+    c->waited = true;
+    ProfScope ps_(c, K_FWT_REV_CHAIN, 16.0 * h);
+    hipchk(jwv::launch_fwt_rev_chain(b, use_fma(c), ca, c->stream), "fwt_rev_chain");
+  };
 }
 
 // Resident-pass cap of an FWT axis transform.  Many contiguous signals (2-D
@@ -456,10 +495,19 @@ int fwt_res_cap(int C, int64_t outer) {
 // reverse that reads them next took 123 us/step).
 int store_pol_dir(int rev, bool final = false) { return rev && final ? 2 : 0; }
 
-void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
+// FastWaveletTransform.forward's level loop (FastWaveletTransform.java:90-97)
+// as device passes.  ws: the ping-pong pair for the level approximations.
+Plan fwt_fwd_plan(jwv_ctx* c, const Bank& b, const Axis& a, int level, DevBuf* ws) {
+  Plan p;
   const int nlev = fwd_levels(a.len, b.tw, level);
-  if (nlev == 0) return copy_axis(c, a);
-  if (try_fwd_chain(c, b, a, nlev)) return;
+  if (nlev == 0) {
+    p.push_back({false, 0, [c, a] { copy_axis(c, a); }});
+    return p;
+  }
+  if (auto f = fwd_chain_step(c, b, a, nlev)) {
+    p.push_back({false, 0, f});
+    return p;
+  }
   const int C = col_slab(a.inner), cap = fwt_res_cap(C, a.outer), KM = Geo::fwt_k(C);
   const bool f1 = fast1(b, a, false);
   // levels of the tiled pass at level-input size h: KM, except that on the
@@ -484,7 +532,7 @@ void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
       h >>= K;
       rem -= K;
     }
-    if (need) { grow(c, c->ws[0], need); grow(c, c->ws[1], need); }
+    if (need) { grow(c, ws[0], need); grow(c, ws[1], need); }
   }
   const double* cur = a.src;
   AxisView cv = a.sv;
@@ -496,23 +544,35 @@ void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
     if (f1 && a.outer == 1 && h < a.len && (plan_of(c) & JWV_PLAN_FWD_TAIL) &&
         K >= jwv::kTailKMin && K <= jwv::kTailKMax && rem > K && h % jwv::kTailTB == 0 &&
         (h >> K) <= jwv::kTailCap && ((uintptr_t)cur & 15) == 0) {
-      jwv::TailArgs ta{cur, a.dst, c->ws[pp].p, tail_counter(c), h, K, rem - K};
-      { ProfScope ps_(c, K_FWT_FWD_TAIL, 16.0 * h);
+      double* wsB = ws[pp].p;
+      unsigned* cnt = tail_counter(c);
+      const int hh = h, lc = rem - K;
+      p.push_back({false, 0, [c, &b, cur, a, wsB, cnt, hh, K, lc] {
+        const unsigned nU = (unsigned)(hh / jwv::kTailTB);
+        const jwv::TailArgs ta{cur, a.dst, wsB, cnt, jwv::tail_last_old(c->tail_base, nU),
+                               hh, K, lc};
+        c->tail_dirty = true;
+        ProfScope ps_(c, K_FWT_FWD_TAIL, 16.0 * hh);
         hipchk(use_fma(c) ? jwv::fused::fwt_fwd_tail(b, ta, c->stream)
-                          : jwv::exact::fwt_fwd_tail(b, ta, c->stream), "fwt_fwd_tail"); }
-      return;
+                          : jwv::exact::fwt_fwd_tail(b, ta, c->stream), "fwt_fwd_tail");
+        c->tail_base = jwv::tail_next_base(c->tail_base, nU);
+      }});
+      return p;
     }
     const bool last = K == rem;
-    double* ad = last ? a.dst : c->ws[pp].p;
+    double* ad = last ? a.dst : ws[pp].p;
     const AxisView av = last ? a.dv : cview(h >> K, a.inner);
-    jwv::TileArgs t{cur, cv, nullptr, {}, a.dst, a.dv, ad, av, h, K, a.outer, a.inner,
-                    dma_view(cur, cv, C, a.inner),
-                    Geo::tile_walk(),
-                    first1 && h == a.len && Geo::fwd1_first_t() != Geo::kFwt1T
-                        ? Geo::fwd1_first_t() : 0};
-    { ProfScope ps_(c, h == a.len ? K_FWT_FWD_TILE : K_FWT_FWD_TILE_DEEP,
-                    16.0 * a.outer * h * a.inner);
-      hipchk(jwv::launch_fwt_fwd_tile(b, use_fma(c), C, t, c->stream), "fwt_fwd_tile"); }
+    const jwv::TileArgs t{cur, cv, nullptr, {}, a.dst, a.dv, ad, av, h, K, a.outer, a.inner,
+                          dma_view(cur, cv, C, a.inner),
+                          Geo::tile_walk(),
+                          first1 && h == a.len && Geo::fwd1_first_t() != Geo::kFwt1T
+                              ? Geo::fwd1_first_t() : 0};
+    const int kind = h == a.len ? K_FWT_FWD_TILE : K_FWT_FWD_TILE_DEEP;
+    const double bytes = 16.0 * a.outer * h * a.inner;
+    p.push_back({false, 0, [c, &b, C, t, kind, bytes] {
+      ProfScope ps_(c, kind, bytes);
+      hipchk(jwv::launch_fwt_fwd_tile(b, use_fma(c), C, t, c->stream), "fwt_fwd_tile");
+    }});
     cur = ad;
     cv = av;
     h >>= K;
@@ -520,22 +580,39 @@ void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
     pp ^= 1;
   }
   if (rem > 0) {
-    jwv::ResArgs r{cur, cv, a.dst, a.dv, h, 0, rem, a.outer, a.inner, dma_view(cur, cv, C, a.inner)};
-    { ProfScope ps_(c, K_FWT_FWD_RES, 16.0 * a.outer * h * a.inner);
-    hipchk(jwv::launch_fwt_fwd_res(b, use_fma(c), C, r, c->stream), "fwt_fwd_res"); }
+    const jwv::ResArgs r{cur, cv, a.dst, a.dv, h, 0, rem, a.outer, a.inner,
+                         dma_view(cur, cv, C, a.inner)};
+    const double bytes = 16.0 * a.outer * h * a.inner;
+    p.push_back({true, h, [c, &b, C, r, bytes] {
+      ProfScope ps_(c, K_FWT_FWD_RES, bytes);
+      hipchk(jwv::launch_fwt_fwd_res(b, use_fma(c), C, r, c->stream), "fwt_fwd_res");
+    }});
   }
+  return p;
 }
 
-void fwt_rev_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
+void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
+  run_plan(fwt_fwd_plan(c, b, a, level, c->ws));
+}
+
+// FastWaveletTransform.reverse's level loop (FastWaveletTransform.java:137-149).
+Plan fwt_rev_plan(jwv_ctx* c, const Bank& b, const Axis& a, int level, DevBuf* ws) {
+  Plan p;
   const int h = rev_first(a.len, b.tw, level);
-  if (h == 0) return copy_axis(c, a);
-  if (try_rev_chain(c, b, a, h)) return;
+  if (h == 0) {
+    p.push_back({false, 0, [c, a] { copy_axis(c, a); }});
+    return p;
+  }
+  if (auto f = rev_chain_step(c, b, a, h)) {
+    p.push_back({false, 0, f});
+    return p;
+  }
   const int C = col_slab(a.inner);
   // fwt1 path, signal longer than one resident block: the resident tail stops
   // at kFwt1RevTail and the tiled passes take up to kFwt1KMax levels
   const bool f1 = fast1(b, a, true) && a.len > fwt_res_cap(C, a.outer);
-  // batches of rows: the resident part stops at rev_row_tail() (env
-  // JWV_REVROWTAIL), one long signal at kFwt1RevTail (the REV_HEAD plan)
+  // batches of rows: the resident part stops at rev_row_tail(), one long
+  // signal at kFwt1RevTail (the REV_HEAD plan)
   const int cap = f1 ? (a.outer > 1 ? rev_row_tail() : Geo::kFwt1RevTail) : Geo::res_cap(C);
   const int KM = f1 ? Geo::kFwt1KMax : Geo::fwt_k(C);
   // workspace sizing
@@ -555,7 +632,7 @@ void fwt_rev_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
       if (hK < a.len) need = std::max(need, (size_t)a.outer * hK * a.inner);
       h1 = hK * 2;
     }
-    if (need) { grow(c, c->ws[0], need); grow(c, c->ws[1], need); }
+    if (need) { grow(c, ws[0], need); grow(c, ws[1], need); }
   }
   const double* acur;
   AxisView acv;
@@ -568,11 +645,13 @@ void fwt_rev_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
       ((int64_t)cap << ChainGeo::kKM) <= a.len) {
     const int hM = cap << ChainGeo::kKM;
     const bool last = hM == a.len;
-    double* out = last ? a.dst : c->ws[1].p;
-    jwv::RevHeadArgs ra{a.src, out, h, exponent(cap / h) + 1};
-    { ProfScope ps_(c, K_FWT_REV_HEAD, 16.0 * hM);
-      hipchk(jwv::launch_fwt_rev_head(b, use_fma(c), ra, c->stream), "fwt_rev_head"); }
-    if (last) return;
+    double* out = last ? a.dst : ws[1].p;
+    const jwv::RevHeadArgs ra{a.src, out, h, exponent(cap / h) + 1};
+    p.push_back({false, 0, [c, &b, ra, hM] {
+      ProfScope ps_(c, K_FWT_REV_HEAD, 16.0 * hM);
+      hipchk(jwv::launch_fwt_rev_head(b, use_fma(c), ra, c->stream), "fwt_rev_head");
+    }});
+    if (last) return p;
     acur = out;
     acv = cview(hM, 1);
     h1 = hM * 2;
@@ -580,13 +659,16 @@ void fwt_rev_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
     const int hres = std::min(a.len, cap);
     const int nres = exponent(hres / h) + 1;
     const bool last = hres == a.len;
-    double* out = last ? a.dst : c->ws[pp].p;
+    double* out = last ? a.dst : ws[pp].p;
     const AxisView ov = last ? a.dv : cview(hres, a.inner);
-    jwv::ResArgs r{a.src, a.sv, out, ov, h, 0, nres, a.outer, a.inner,
-                   dma_view(a.src, a.sv, C, a.inner)};
-    { ProfScope ps_(c, K_FWT_REV_RES, 16.0 * a.outer * hres * a.inner);
-    hipchk(jwv::launch_fwt_rev_res(b, use_fma(c), C, r, c->stream), "fwt_rev_res"); }
-    if (last) return;
+    const jwv::ResArgs r{a.src, a.sv, out, ov, h, 0, nres, a.outer, a.inner,
+                         dma_view(a.src, a.sv, C, a.inner)};
+    const double bytes = 16.0 * a.outer * hres * a.inner;
+    p.push_back({true, hres, [c, &b, C, r, bytes] {
+      ProfScope ps_(c, K_FWT_REV_RES, bytes);
+      hipchk(jwv::launch_fwt_rev_res(b, use_fma(c), C, r, c->stream), "fwt_rev_res");
+    }});
+    if (last) return p;
     acur = out;
     acv = ov;
     h1 = hres * 2;
@@ -600,19 +682,28 @@ void fwt_rev_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
     const int K = std::min(exponent(a.len / h1) + 1, KM);
     const int hK = h1 << (K - 1);
     const bool last = hK == a.len;
-    double* out = last ? a.dst : c->ws[pp].p;
+    double* out = last ? a.dst : ws[pp].p;
     const AxisView ov = last ? a.dv : cview(hK, a.inner);
-    jwv::TileArgs t{acur, acv, a.src, a.sv, out, ov, nullptr, {}, h1, K, a.outer, a.inner,
-                    dma_view(acur, acv, C, a.inner) && dma_view(a.src, a.sv, C, a.inner),
-                    (last ? store_pol_dir(1, a.outer == 1 && a.inner == 1) : 0) |
-                        Geo::tile_walk()};
-    { ProfScope ps_(c, last ? K_FWT_REV_TILE : K_FWT_REV_TILE_DEEP, 16.0 * a.outer * hK * a.inner);
-    hipchk(jwv::launch_fwt_rev_tile(b, use_fma(c), C, t, c->stream), "fwt_rev_tile"); }
+    const jwv::TileArgs t{acur, acv, a.src, a.sv, out, ov, nullptr, {}, h1, K, a.outer, a.inner,
+                          dma_view(acur, acv, C, a.inner) && dma_view(a.src, a.sv, C, a.inner),
+                          (last ? store_pol_dir(1, a.outer == 1 && a.inner == 1) : 0) |
+                              Geo::tile_walk()};
+    const int kind = last ? K_FWT_REV_TILE : K_FWT_REV_TILE_DEEP;
+    const double bytes = 16.0 * a.outer * hK * a.inner;
+    p.push_back({false, 0, [c, &b, C, t, kind, bytes] {
+      ProfScope ps_(c, kind, bytes);
+      hipchk(jwv::launch_fwt_rev_tile(b, use_fma(c), C, t, c->stream), "fwt_rev_tile");
+    }});
     acur = out;
     acv = ov;
     h1 = hK * 2;
     pp ^= 1;
   }
+  return p;
+}
+
+void fwt_rev_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
+  run_plan(fwt_rev_plan(c, b, a, level, c->ws));
 }
 
 // ------------------------------------------------------------------ WPT axis
@@ -787,10 +878,13 @@ int guarded(jwv_ctx* c, F&& f) {
     c->err.clear();
     DeviceScope ds(c->device);
     f();
+    c->tail_dirty = false;
     return JWV_OK;
   } catch (const Fail& e) {
+    tail_resync(c);
     return set_err(c, e.code, e.msg);
   } catch (const std::exception& e) {
+    tail_resync(c);
     return set_err(c, JWV_ERR_DEVICE, e.what());
   }
 }
@@ -925,12 +1019,173 @@ AxisFn axis_fn(Kind k, bool fwd) {
   return fwd ? wpt_fwd_axis : wpt_rev_axis;
 }
 
+// ---- overlapped 2-D FWT schedule
+// The resident passes (the latency-bound tails of each axis: one block per
+// row or column slab, a chain of levels with a barrier each) leave most of
+// the chip's HBM bandwidth idle.  They only touch part of the matrix, so
+// they can run beside the HBM-bound tile passes of the columns that do not
+// depend on them:
+//   forward  rows (tiles -> resident), then columns.  The row resident pass
+//            writes columns [0, hr) only; the column passes of [hr, cols) run
+//            beside it.  Each column group's resident pass runs on a side
+//            stream beside the next group's tiles.
+//   reverse  columns (resident -> tiles), then rows.  The row resident pass
+//            reads columns [0, hres) only: it runs beside the column tiles of
+//            [hres, cols) once group [0, hres) is done.  The column resident
+//            passes run ahead on a side stream.
+// Every column runs exactly the kernels of the serial schedule (its own
+// plan), so the result is bit-identical; only launch order and streams
+// differ.  Groups are multiples of 128 columns (whole XCD-paired slabs).
+#ifndef JWV_2D_OVERLAP
+#define JWV_2D_OVERLAP 1
+#endif
+#ifndef JWV_2D_GROUPS
+#define JWV_2D_GROUPS 4
+#endif
+#ifndef JWV_SIDE_PRIO
+#define JWV_SIDE_PRIO 1
+#endif
+constexpr int kOverlapMinElems = 1 << 22;
+constexpr int kColUnit = 128;
+constexpr size_t kEvRing = 64;
+
+hipStream_t side_stream(jwv_ctx* c, int i) {
+  if (!c->side[i]) {
+    int least = 0, greatest = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIPCHK(hipStreamCreateWithPriority(&c->side[i], hipStreamNonBlocking,
+                                       JWV_SIDE_PRIO ? greatest : least));
+  }
+  return c->side[i];
+}
+// An ordering event recorded on s.  The ring is reused call after call: a
+// wait keeps the record it was enqueued against, so re-recording later is safe.
+hipEvent_t mark(jwv_ctx* c, hipStream_t s) {
+  hipEvent_t e;
+  if (c->xev.size() < kEvRing) {
+    hipchk(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    c->xev.push_back(e);
+  } else {
+    e = c->xev[c->xev_next++ % kEvRing];
+  }
+  hipchk(hipEventRecord(e, s), "hipEventRecord");
+  return e;
+}
+void wait_on(hipStream_t s, hipEvent_t e) { hipchk(hipStreamWaitEvent(s, e, 0), "hipStreamWaitEvent"); }
+// run f with s as the launch stream
+void on_stream(jwv_ctx* c, hipStream_t s, const std::function<void()>& f) {
+  hipStream_t keep = c->stream;
+  c->stream = s;
+  try {
+    f();
+  } catch (...) {
+    c->stream = keep;
+    throw;
+  }
+  c->stream = keep;
+}
+
+struct ColGroup {
+  int c0, w;
+  Plan p;
+};
+// [lo, hi) as up to n groups of whole kColUnit-column units
+void split_cols(std::vector<ColGroup>& out, int lo, int hi, int n) {
+  const int units = (hi - lo) / kColUnit;
+  n = std::max(1, std::min(n, units));
+  for (int i = 0; i < n; ++i) {
+    const int a = lo + (int)((int64_t)units * i / n) * kColUnit;
+    const int e = i + 1 == n ? hi : lo + (int)((int64_t)units * (i + 1) / n) * kColUnit;
+    out.push_back({a, e - a, {}});
+  }
+}
+
+bool body_2d_fwt(jwv_ctx* c, bool fwd, const Bank& b, const double* x, double* y, double* tmp,
+                 int64_t rows, int64_t cols, int lvl_m, int lvl_n) {
+  if (!JWV_2D_OVERLAP || rows * cols < kOverlapMinElems || cols % kColUnit) return false;
+  const AxisView rv = cview(cols, 1), cvw = cview(rows, cols);
+  // plans first (they allocate), launches after
+  Plan R = fwd ? fwt_fwd_plan(c, b, Axis{x, rv, tmp, rv, rows, (int)cols, 1}, lvl_n, c->ws)
+               : fwt_rev_plan(c, b, Axis{tmp, rv, y, rv, rows, (int)cols, 1}, lvl_n, c->ws);
+  const Step* rres = nullptr;
+  if (!R.empty() && (fwd ? R.back().res : R.front().res)) rres = fwd ? &R.back() : &R.front();
+  const int hr = rres ? rres->h : 0;  // columns the row resident pass touches
+  if (hr % kColUnit || hr >= cols) return false;
+  std::vector<ColGroup> g;
+  if (hr) g.push_back({0, hr, {}});
+  split_cols(g, hr, (int)cols, JWV_2D_GROUPS);
+  if (c->gws.size() < 2 * g.size()) c->gws.resize(2 * g.size());
+  for (size_t i = 0; i < g.size(); ++i) {
+    const double* src = fwd ? tmp + g[i].c0 : x + g[i].c0;
+    double* dst = fwd ? y + g[i].c0 : tmp + g[i].c0;
+    const Axis a{src, cvw, dst, cvw, 1, (int)rows, g[i].w};
+    g[i].p = fwd ? fwt_fwd_plan(c, b, a, lvl_m, &c->gws[2 * i])
+                 : fwt_rev_plan(c, b, a, lvl_m, &c->gws[2 * i]);
+  }
+  hipStream_t s0 = c->stream, s1 = side_stream(c, 0), s2 = side_stream(c, 1);
+  if (fwd) {
+    for (const Step& s : R)
+      if (&s != rres) s.go();
+    hipEvent_t er = nullptr;
+    if (rres) {
+      wait_on(s2, mark(c, s0));
+      on_stream(c, s2, rres->go);
+      er = mark(c, s2);
+    }
+    // group order: the first independent group, then [0, hr) (its row
+    // resident pass has had one group's time to finish), then the rest
+    std::vector<size_t> order;
+    for (size_t i = hr ? 1 : 0; i < g.size(); ++i) {
+      order.push_back(i);
+      if (hr && i == 1) order.push_back(0);
+    }
+    if (hr && g.size() == 1) order.push_back(0);
+    for (size_t i : order) {
+      if (hr && i == 0) wait_on(s0, er);
+      const Plan& p = g[i].p;
+      const bool tail = p.back().res;
+      for (size_t k = 0; k + (tail ? 1 : 0) < p.size(); ++k) p[k].go();
+      if (tail) {
+        wait_on(s1, mark(c, s0));
+        on_stream(c, s1, p.back().go);
+      }
+    }
+    wait_on(s0, mark(c, s1));
+    if (er) wait_on(s0, er);
+  } else {
+    wait_on(s1, mark(c, s0));
+    std::vector<hipEvent_t> ea(g.size(), nullptr);
+    for (size_t i = 0; i < g.size(); ++i)
+      if (g[i].p.front().res) {
+        on_stream(c, s1, g[i].p.front().go);
+        ea[i] = mark(c, s1);
+      }
+    hipEvent_t er = nullptr;
+    for (size_t i = 0; i < g.size(); ++i) {
+      const Plan& p = g[i].p;
+      if (ea[i]) wait_on(s0, ea[i]);
+      for (size_t k = ea[i] ? 1 : 0; k < p.size(); ++k) p[k].go();
+      if (hr && i == 0) {
+        wait_on(s2, mark(c, s0));
+        on_stream(c, s2, rres->go);
+        er = mark(c, s2);
+      }
+    }
+    wait_on(s0, mark(c, s1));
+    if (er) wait_on(s0, er);
+    for (const Step& s : R)
+      if (&s != rres) s.go();
+  }
+  return true;
+}
+
 // BasicTransform.java:361-399 (forward: rows lvlN -> columns lvlM) and
 // :436-474 (reverse: columns lvlM -> rows lvlN).
 void body_2d(jwv_ctx* c, Kind k, bool fwd, const Bank& b, const double* x, double* y,
              int64_t rows, int64_t cols, int lvl_m, int lvl_n) {
   if (rows == 0 || cols == 0) return;
   double* tmp = grow(c, c->big, (size_t)(rows * cols));
+  if (k == Kind::FWT && body_2d_fwt(c, fwd, b, x, y, tmp, rows, cols, lvl_m, lvl_n)) return;
   const AxisView rv = cview(cols, 1), cvw = cview(rows, cols);
   AxisFn f = axis_fn(k, fwd);
   if (fwd) {
@@ -1345,6 +1600,11 @@ int jwv_ctx_destroy(jwv_ctx* c) {
   if (c->sync) hipFree(c->sync);
   for (auto& r : c->recs) { hipEventDestroy(r.e0); hipEventDestroy(r.e1); }
   for (auto e : c->ev_pool) hipEventDestroy(e);
+  for (auto e : c->xev) hipEventDestroy(e);
+  for (DevBuf& b : c->gws)
+    if (b.p) hipFree(b.p);
+  for (hipStream_t s : c->side)
+    if (s) hipStreamDestroy(s);
   for (int i = 0; i < kPinSlots; ++i) {
     if (c->pin.p[i]) hipHostFree(c->pin.p[i]);
     if (c->pin.ev[i]) hipEventDestroy(c->pin.ev[i]);
@@ -1457,6 +1717,9 @@ int jwv_ctx_trim(jwv_ctx* c) {
       b->p = nullptr;
       b->n = 0;
     }
+    for (DevBuf& g : c->gws)
+      if (g.p) hipchk(hipFree(g.p), "free");
+    c->gws.clear();
   });
 }
 

@@ -258,15 +258,16 @@ __global__ __launch_bounds__(NT, MINW) void fwt_rev_chain1(const double* __restr
 // Forward tail: B units (tiles of TB level-input samples, KB levels; input =
 // the big pass's approximation, written by the previous launch) and, in the
 // block that completes the counter, the resident C levels.  Grid: hB / TB.
-// cnt[0]: arrival counter, reset by the last arriver.
+// cnt[0]: arrival counter, never reset; the block whose add returns last_old
+// is the last arriver (jwv_epoch.hpp).
 template <int L, int NT, int TB, int KB, int CAPC, bool FMA>
 __global__ __launch_bounds__(NT) void fwt_fwd_tail1(const double* __restrict__ src,
                                                     double* __restrict__ dst, double* wsB,
-                                                    unsigned* cnt, int hB, int levC,
-                                                    FwdTaps<L> tp) {
+                                                    unsigned* cnt, unsigned last_old, int hB,
+                                                    int levC, FwdTaps<L> tp) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   using GB = Fwd1Geo<L, TB, KB>;
-  const int tid = threadIdx.x, u = blockIdx.x, nU = gridDim.x;
+  const int tid = threadIdx.x, u = blockIdx.x;
   int* ctl = reinterpret_cast<int*>(lds + tail_ctl_off<L, TB, KB>(hB >> KB));
   {
     const int msk = hB - 1, base = u * TB;
@@ -278,10 +279,7 @@ __global__ __launch_bounds__(NT) void fwt_fwd_tail1(const double* __restrict__ s
   drain_stores();
   __syncthreads();
   if (tid == 0) {
-    const unsigned old = atomic_add_agent(cnt, 1u);
-    const int last = old == (unsigned)nU - 1;
-    if (last) store_agent(cnt, 0u);
-    ctl[0] = last;
+    ctl[0] = atomic_add_agent(cnt, 1u) == last_old;
   }
   __syncthreads();
   if (!ctl[0]) return;

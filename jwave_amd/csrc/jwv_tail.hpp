@@ -1,6 +1,7 @@
 // jwv_tail.hpp — host entry points of launch_tail.hip, one per math mode:
 // the fused forward tail (fwt_fwd_tail1, fwt1_chain.hpp).
 #pragma once
+#include "jwv_epoch.hpp"
 #include "jwv_launch.hpp"
 
 namespace jwv {
@@ -14,7 +15,8 @@ struct TailArgs {
   const double* src;   // level input, length hB (the first pass's approximation)
   double* dst;         // the signal's coefficient array
   double* wsB;         // hB >> kTailKB doubles (handed to the last unit)
-  unsigned* cnt;       // one word, zero between calls (reset by the last unit)
+  unsigned* cnt;       // arrival counter (never reset, jwv_epoch.hpp)
+  unsigned last_old;   // tail_last_old(counter value at launch, hB / kTailTB)
   int hB, KB, levC;
 };
 constexpr int kTailTB = 2048, kTailKMin = 6, kTailKMax = 9, kTailCap = 1024;

@@ -32,7 +32,7 @@ hipError_t tail_k(const Bank& b, const TailArgs& a, hipStream_t s) {
   FwdTaps<L> tp;
   for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
   JWV_LAUNCH(k, dim3((unsigned)(a.hB / kTailTB)), dim3(NT), lds, s, a.src, a.dst, a.wsB,
-                     a.cnt, a.hB, a.levC, tp);
+                     a.cnt, a.last_old, a.hB, a.levC, tp);
   return hipGetLastError();
 }
 template <int L>

@@ -319,6 +319,32 @@ def test_fwt2d_rowcap(ctx, ctx_fma, wname, shape):
             assert_close(T.transform_2d(yr, w, lm, ln, False, ctx_fma), xr, "2d rev fma")
 
 
+@pytest.mark.parametrize("wname", ["Haar1", "Daubechies2", "Daubechies4", "Daubechies8"])
+@pytest.mark.parametrize("shape", [(2048, 2048), (512, 8192), (1024, 4096), (8192, 512),
+                                   (4096, 1024)])
+def test_fwt2d_overlapped_schedule(ctx, ctx_fma, wname, shape):
+    """Matrices of >= 2^22 elements take the overlapped 2-D schedule
+    (capi.cpp body_2d_fwt): row / column resident passes on side streams
+    beside the tile passes of independent column groups.  Every column runs
+    its serial plan, so the result must stay bit-exact at full and partial
+    levels on both axes (partial levels move or remove the resident passes
+    and the group [0, hr))."""
+    w = jw.by_class(wname)
+    r, c = shape
+    x = rnd(r * c, r + 3 * c).reshape(r, c)
+    fm, fn = r.bit_length() - 1, c.bit_length() - 1
+    for lm, ln in ((fm, fn), (3, fn), (fm, 2), (0, fn), (fm, 0), (fm - 1, fn - 3)):
+        yr = oracle.transform_2d("fwt", True, w, x, lm, ln)
+        assert_exact(T.transform_2d(x, w, lm, ln, True, ctx), yr,
+                     "2d fwd %s %s l=(%d,%d)" % (wname, shape, lm, ln))
+        xr = oracle.transform_2d("fwt", False, w, yr, lm, ln)
+        assert_exact(T.transform_2d(yr, w, lm, ln, False, ctx), xr,
+                     "2d rev %s %s l=(%d,%d)" % (wname, shape, lm, ln))
+        if (lm, ln) == (fm, fn) and wname == "Daubechies8":
+            assert_close(T.transform_2d(x, w, lm, ln, True, ctx_fma), yr, "2d fwd fma")
+            assert_close(T.transform_2d(yr, w, lm, ln, False, ctx_fma), xr, "2d rev fma")
+
+
 @pytest.mark.parametrize("wname", ["Haar1", "Daubechies2", "Daubechies4", "Daubechies8", "Symlet8"])
 def test_fwt_batch_rowcap(ctx, wname):
     """Batched 1-D FWT, 64 signals x 8192 (>= 64 rows, > 2048 samples: the

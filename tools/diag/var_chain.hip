@@ -102,8 +102,11 @@ static void fwd_split() {
   const size_t l2 = ((size_t)tail_ctl_off<8, 2048, KB>(CAPC) + 2) * 8;
   big_lds(k2, l2);
   hipLaunchKernelGGL(k1, dim3(H / 2048), dim3(256), l1, 0, x, 0, y, 0, wa, 0, H, tf);
-  hipLaunchKernelGGL(k2, dim3((H >> 6) / 2048), dim3(256), l2, 0, wa, y, wb, sync_ + 8000, H >> 6,
-                     24 - 6 - KB, tf);
+  static unsigned base = 0;  // arrival counter value (jwv_epoch.hpp)
+  const unsigned nU = (H >> 6) / 2048;
+  hipLaunchKernelGGL(k2, dim3(nU), dim3(256), l2, 0, wa, y, wb, sync_ + 8000, base + nU - 1,
+                     H >> 6, 24 - 6 - KB, tf);
+  base += nU;
 }
 static double* wr;
 static void rev_split() {
