@@ -90,8 +90,9 @@ int jwv_ctx_set_math(jwv_ctx* ctx, int mode);
  * JWV_PLAN_FWD_TAIL: the forward's deep tiled pass and its resident pass in
  * one launch (the unit that completes an arrival counter runs the resident
  * levels; no wait).
- * Default: JWV_PLAN_REV_HEAD | JWV_PLAN_FWD_TAIL (env JWV_PLAN overrides the
- * default flags). */
+ * Default: JWV_PLAN_REV_HEAD | JWV_PLAN_FWD_TAIL (jwv_ctx_set_plan is the only
+ * way to change it; the library reads no environment setting but the
+ * JWV_LAUNCH_LOG diagnostic). */
 #define JWV_PLAN_CHAIN_REV 1
 #define JWV_PLAN_CHAIN_FWD 2
 #define JWV_PLAN_REV_HEAD 4
@@ -120,7 +121,15 @@ int jwv_ctx_profile_enable(jwv_ctx* ctx, int on);
 int jwv_ctx_profile_read(jwv_ctx* ctx, jwv_kernel_stat* out, int max_out, int* n_out);
 /* Restrict profiling events to one kernel kind (by name; NULL or "" = all). */
 int jwv_ctx_profile_select(jwv_ctx* ctx, const char* kind);
-/* Release cached device workspace. */
+/* Release cached device workspace and the pinned staging ring.
+ * A context owns its workspace and its fused-tail arrival counters: it runs
+ * one transform at a time (calls on one context are
+ * serialised), and work it queued on one stream must have completed before
+ * the context is pointed at another stream (jwv_ctx_set_stream) whose work is
+ * not ordered after it.  Footprint: device workspace as large as the largest
+ * transform's intermediates (one matrix for 2-D / 3-D), plus, once a host
+ * entry staged pageable memory, 4 x 32 MiB of pinned host memory; the host
+ * copy threads are one process-wide pool. */
 int jwv_ctx_trim(jwv_ctx* ctx);
 
 /* Page-locked host memory for the host-pointer entry points.  The host entry
@@ -165,6 +174,41 @@ int jwv_fwt_fwd_batch_f64_dev(const double* x, double* y, int64_t batch, int64_t
                               int level, const jwv_taps* t, jwv_ctx* ctx);
 int jwv_fwt_rev_batch_f64_dev(const double* y, double* x, int64_t batch, int64_t n, int64_t ld,
                               int level, const jwv_taps* t, jwv_ctx* ctx);
+
+/* ---- multi-device batches ---------------------------------------------------
+ * One context per listed device (duplicates allowed).  The batched host
+ * entries split the batch into contiguous blocks of signals, device i taking
+ * signals [start_i, start_i + count_i) of jwv_batch_split(batch, n, i), and
+ * run the blocks concurrently, one host thread per device (stage in,
+ * transform, stage out on that device's stream): no collective, every device
+ * its own PCIe link.  They return when every device has finished; arguments
+ * are validated once, with the single-device messages, before any device
+ * starts; a device failure returns that device's status and message
+ * (jwv_mctx_last_error; the lowest failing device index wins).  Results are
+ * those of the single-device batched entries, signal for signal.
+ * Reference: the executor over independent signals of
+ * src/test/java/jwave/ParallelizationOpportunityTest.java:80-98, spread over the
+ * node's GPUs. */
+typedef struct jwv_mctx jwv_mctx;
+int jwv_mctx_create(const int* devices, int n_devices, jwv_mctx** out);
+int jwv_mctx_destroy(jwv_mctx* m);
+const char* jwv_mctx_last_error(const jwv_mctx* m);
+int jwv_mctx_size(const jwv_mctx* m);
+/* the per-device context i (profiling, streams, trim); owned by m */
+jwv_ctx* jwv_mctx_ctx(jwv_mctx* m, int i);
+int jwv_mctx_set_math(jwv_mctx* m, int mode);
+/* Contiguous block of device i (0 <= i < n_devices) in a batch of `batch`:
+ * start = floor(batch*i/n), count = floor(batch*(i+1)/n) - start.  Pure
+ * arithmetic, no device needed. */
+int jwv_batch_split(int64_t batch, int n_devices, int i, int64_t* start, int64_t* count);
+int jwv_m_fwt_fwd_batch_f64(const double* x, double* y, int64_t batch, int64_t n, int64_t ld,
+                            int level, const jwv_taps* t, jwv_mctx* m);
+int jwv_m_fwt_rev_batch_f64(const double* y, double* x, int64_t batch, int64_t n, int64_t ld,
+                            int level, const jwv_taps* t, jwv_mctx* m);
+int jwv_m_wpt_fwd_batch_f64(const double* x, double* y, int64_t batch, int64_t n, int64_t ld,
+                            int level, const jwv_taps* t, jwv_mctx* m);
+int jwv_m_wpt_rev_batch_f64(const double* y, double* x, int64_t batch, int64_t n, int64_t ld,
+                            int level, const jwv_taps* t, jwv_mctx* m);
 
 /* ---- 2-D / 3-D FWT -----------------------------------------------------------
  * BasicTransform.forward(double[][], lvlM, lvlN)  BasicTransform.java:361-399

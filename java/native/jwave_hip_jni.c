@@ -315,3 +315,55 @@ JNIEXPORT jint JNICALL Java_jwave_amd_HipNative_decompose(
   TAPS(B);
   STAGED(jx, n, jmat, nm, { rc = jwv_decompose_f64(x, y, n, kind, t, CTX(ctx)); });
 }
+
+/* ---- multi-device batches (jwv_mctx; HipNative.mctx, jwave.hip.devices) ---- */
+#define MCTX(h) ((jwv_mctx*)(intptr_t)(h))
+
+JNIEXPORT jint JNICALL Java_jwave_amd_HipNative_mctxCreate(JNIEnv* env, jclass cls,
+                                                           jintArray jdev, jlongArray out) {
+  const jsize n = (*env)->GetArrayLength(env, jdev);
+  if (n < 1 || n > 1024) {
+    throw_java(env, "java/lang/IllegalArgumentException", "jwave_hip_jni: 1..1024 devices");
+    return STAGE_FAIL;
+  }
+  jint dev[1024];
+  (*env)->GetIntArrayRegion(env, jdev, 0, n, dev);
+  if ((*env)->ExceptionCheck(env)) return STAGE_FAIL;
+  int d[1024];
+  for (jsize i = 0; i < n; ++i) d[i] = (int)dev[i];
+  jwv_mctx* m = NULL;
+  const int rc = jwv_mctx_create(d, (int)n, &m);
+  jlong h = (jlong)(intptr_t)m;
+  (*env)->SetLongArrayRegion(env, out, 0, 1, &h);
+  return rc;
+}
+
+JNIEXPORT jstring JNICALL Java_jwave_amd_HipNative_mctxLastError(JNIEnv* env, jclass cls,
+                                                                 jlong mctx) {
+  return (*env)->NewStringUTF(env, jwv_mctx_last_error(MCTX(mctx)));
+}
+
+/* batched signals split over the devices of a multi-context: staged once
+ * through the calling thread's pinned staging (device 0's context allocates
+ * it; page-locked memory is DMA-able by every device), then one call that
+ * runs every device's block concurrently */
+JNIEXPORT jint JNICALL Java_jwave_amd_HipNative_transformBatchMulti(
+    JNIEnv* env, jclass cls, jlong mctx, jint kind, jboolean fwd, jdoubleArray jx,
+    jdoubleArray jy, jint batch, jint n, jint level, jint L, jint tw, jdouble scale,
+    jdoubleArray jlo, jdoubleArray jhi, jdoubleArray jlor, jdoubleArray jhir) {
+  const int64_t tot = (int64_t)batch * n;
+  const jlong ctx = (jlong)(intptr_t)jwv_mctx_ctx(MCTX(mctx), 0);
+  if (!ctx) {
+    throw_java(env, "java/lang/IllegalArgumentException", "jwave_hip_jni: no multi-context");
+    return STAGE_FAIL;
+  }
+  TAPS(B);
+  STAGED(jx, tot, jy, tot, {
+    if (kind == 0)
+      rc = fwd ? jwv_m_fwt_fwd_batch_f64(x, y, batch, n, n, level, t, MCTX(mctx))
+               : jwv_m_fwt_rev_batch_f64(x, y, batch, n, n, level, t, MCTX(mctx));
+    else
+      rc = fwd ? jwv_m_wpt_fwd_batch_f64(x, y, batch, n, n, level, t, MCTX(mctx))
+               : jwv_m_wpt_rev_batch_f64(x, y, batch, n, n, level, t, MCTX(mctx));
+  });
+}

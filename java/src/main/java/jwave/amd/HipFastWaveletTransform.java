@@ -67,6 +67,27 @@ public class HipFastWaveletTransform extends FastWaveletTransform implements Hip
     return HipNative.unpack( mat, rows, n );
   }
 
+  /** Every row (one signal each, equal lengths) with the same level: one
+   *  native call, split over the GPUs of -Djwave.hip.devices when set. */
+  public double[ ][ ] forwardBatch( double[ ][ ] signals, int level ) throws JWaveException {
+    return batch( true, signals, level );
+  }
+
+  public double[ ][ ] reverseBatch( double[ ][ ] coeffs, int level ) throws JWaveException {
+    return batch( false, coeffs, level );
+  }
+
+  private double[ ][ ] batch( boolean fwd, double[ ][ ] m, int level ) throws JWaveException {
+    int rows = m.length, cols = rows == 0 ? 0 : m[ 0 ].length;
+    if( _taps == null || !HipNative.fitsArray( rows, cols ) ) {
+      double[ ][ ] out = new double[ rows ][ ];
+      for( int i = 0; i < rows; i++ )
+        out[ i ] = fwd ? forward( m[ i ], level ) : reverse( m[ i ], level );
+      return out;
+    }
+    return HipNative.batch( _kind, _taps, fwd, m, level );
+  }
+
   /** The bank this transform sends to the GPU, or null (Java fallback). */
   @Override public HipNative.Taps taps( ) { return _taps; }
 

@@ -34,6 +34,64 @@ public final class HipNative {
 
   static long ctx( ) { return CTX.get( ); }
 
+  // Multi-device batches: -Djwave.hip.devices=0,1,...,7 spreads the batched
+  // entries (forwardBatch / reverseBatch) over those GPUs, one contiguous
+  // block of signals per device (jwv_mctx, include/jwave_hip.h), as the
+  // reference's executor spreads independent signals over threads
+  // (src/test/java/jwave/ParallelizationOpportunityTest.java:80-98).  Unset
+  // or one device: the calling thread's single-device context.  One
+  // multi-context per process (its calls are serialised; each runs one host
+  // thread per device).
+  private static long MCTX = -1L;
+
+  static synchronized long mctx( ) {
+    if( MCTX >= 0 )
+      return MCTX;
+    MCTX = 0L;
+    String p = System.getProperty( "jwave.hip.devices" );
+    if( p == null || p.trim( ).isEmpty( ) )
+      return MCTX;
+    String[ ] parts = p.trim( ).split( "\\s*,\\s*" );
+    if( parts.length < 2 )
+      return MCTX;
+    int[ ] dev = new int[ parts.length ];
+    for( int i = 0; i < dev.length; i++ )
+      dev[ i ] = Integer.parseInt( parts[ i ] );
+    long[ ] h = new long[ 1 ];
+    int rc = mctxCreate( dev, h );
+    if( rc != OK )
+      throw new IllegalStateException( mctxLastError( 0L ) );
+    MCTX = h[ 0 ];
+    return MCTX;
+  }
+
+  static void checkMulti( long m, int rc ) throws JWaveException {
+    if( rc == OK )
+      return;
+    String msg = mctxLastError( m );
+    switch( rc ) {
+      case FAILURE:          throw new JWaveFailure( msg );
+      case ILLEGAL_ARGUMENT: throw new IllegalArgumentException( msg );
+      default:               throw new JWaveError( msg );
+    }
+  }
+
+  /** Every row of m (equal lengths) with the same level in one native call:
+   *  over the jwave.hip.devices GPUs when set, else this thread's device. */
+  static double[ ][ ] batch( int kind, Taps t, boolean fwd, double[ ][ ] m, int level )
+      throws JWaveException {
+    int rows = m.length, cols = rows == 0 ? 0 : m[ 0 ].length;
+    double[ ] x = pack( m ), y = new double[ x.length ];
+    long mc = mctx( );
+    if( mc != 0L )
+      checkMulti( mc, transformBatchMulti( mc, kind, fwd, x, y, rows, cols, level, t.L, t.tw,
+          t.scale, t.lo, t.hi, t.loR, t.hiR ) );
+    else
+      check( transformBatch( ctx( ), kind, fwd, x, y, rows, cols, level, t.L, t.tw, t.scale,
+          t.lo, t.hi, t.loR, t.hiR ) );
+    return unpack( y, rows, cols );
+  }
+
   /** Filter bank as passed to every call: {L, tw, scale} + 4 tap arrays. */
   static final class Taps {
     final int L, tw;
@@ -96,6 +154,14 @@ public final class HipNative {
   static native int transform1d( long ctx, int kind, boolean forward, double[ ] x, double[ ] y,
       int level, int L, int tw, double scale, double[ ] lo, double[ ] hi, double[ ] loR,
       double[ ] hiR );
+
+  static native int mctxCreate( int[ ] devices, long[ ] out );
+  static native String mctxLastError( long mctx );
+
+  /** transformBatch over the devices of a multi-context (jwv_m_*_batch_f64). */
+  static native int transformBatchMulti( long mctx, int kind, boolean forward, double[ ] x,
+      double[ ] y, int batch, int n, int level, int L, int tw, double scale, double[ ] lo,
+      double[ ] hi, double[ ] loR, double[ ] hiR );
 
   /** batch signals of length n, packed contiguously (ld = n). */
   static native int transformBatch( long ctx, int kind, boolean forward, double[ ] x,

@@ -76,8 +76,12 @@ public class HipParallelTransform extends ParallelTransform {
     return m.length < MIN_PARALLEL_SIZE || m[ 0 ].length < MIN_PARALLEL_SIZE;
   }
 
+  // the reference's tasks wrap the cause in a RuntimeException (ParallelTransform.java:259-269),
+  // whose message is the cause's Throwable.toString(); a ForkJoin re-wrap on a
+  // pool worker ("java.lang.RuntimeException: ...") is scheduling-dependent and
+  // not reproduced
   private static JWaveException wrap( String what, JWaveException e ) {
-    return new JWaveException( "Error in parallel " + what + " transform: " + e.getMessage( ) );
+    return new JWaveException( "Error in parallel " + what + " transform: " + e.toString( ) );
   }
 
   @Override public double[ ][ ] forward( double[ ][ ] m, int lvlM, int lvlN )

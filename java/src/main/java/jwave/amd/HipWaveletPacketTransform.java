@@ -83,7 +83,8 @@ public class HipWaveletPacketTransform extends WaveletPacketTransform implements
   }
 
   /** Every row (one signal each, equal lengths) with the same level: one
-   *  native call instead of one per signal. */
+   *  native call instead of one per signal, split over the GPUs listed in
+   *  -Djwave.hip.devices when set (HipNative.batch). */
   public double[ ][ ] forwardBatch( double[ ][ ] signals, int level ) throws JWaveException {
     return batch( true, signals, level );
   }
@@ -100,10 +101,6 @@ public class HipWaveletPacketTransform extends WaveletPacketTransform implements
         out[ i ] = fwd ? super.forward( m[ i ], level ) : super.reverse( m[ i ], level );
       return out;
     }
-    double[ ] x = HipNative.pack( m ), y = new double[ x.length ];
-    HipNative.Taps t = _taps;
-    HipNative.check( HipNative.transformBatch( HipNative.ctx( ), 1, fwd, x, y, rows, cols, level,
-        t.L, t.tw, t.scale, t.lo, t.hi, t.loR, t.hiR ) );
-    return HipNative.unpack( y, rows, cols );
+    return HipNative.batch( 1, _taps, fwd, m, level );
   }
 }

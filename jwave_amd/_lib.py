@@ -110,7 +110,21 @@ for _n in ("modwt_fwd", "modwt_inv"):
     for _s in ("", "_dev"):
         _SIGS["jwv_%s_f64%s" % (_n, _s)] = [_dp, _dp, _i64, _int, _TP, _CTX]
 
-_RESTYPES = {"jwv_last_error": ctypes.c_char_p, "jwv_ctx_get_stream": ctypes.c_void_p}
+_MCTX = ctypes.c_void_p
+_SIGS.update({
+    "jwv_mctx_create": [ctypes.POINTER(_int), _int, ctypes.POINTER(ctypes.c_void_p)],
+    "jwv_mctx_destroy": [_MCTX],
+    "jwv_mctx_last_error": [_MCTX],
+    "jwv_mctx_size": [_MCTX],
+    "jwv_mctx_ctx": [_MCTX, _int],
+    "jwv_mctx_set_math": [_MCTX, _int],
+    "jwv_batch_split": [_i64, _int, _int, ctypes.POINTER(_i64), ctypes.POINTER(_i64)],
+})
+for _n in ("fwt_fwd", "fwt_rev", "wpt_fwd", "wpt_rev"):
+    _SIGS["jwv_m_%s_batch_f64" % _n] = [_dp, _dp, _i64, _i64, _i64, _int, _TP, _MCTX]
+
+_RESTYPES = {"jwv_last_error": ctypes.c_char_p, "jwv_ctx_get_stream": ctypes.c_void_p,
+             "jwv_mctx_last_error": ctypes.c_char_p, "jwv_mctx_ctx": ctypes.c_void_p}
 
 _lib = None
 _lock = threading.Lock()

@@ -21,6 +21,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <condition_variable>
+#include <deque>
 #include <functional>
 #include <mutex>
 #include <sched.h>
@@ -60,20 +61,14 @@ struct DevBuf {
 constexpr size_t kPinChunk = size_t(32) << 20;  // bytes per slot
 constexpr int kPinSlots = 4;
 
-// A few host threads for the pageable <-> pinned copies (one core's memcpy
-// is several times slower than the PCIe link).
+// Host threads for the pageable <-> pinned copies (one core's memcpy is
+// several times slower than the PCIe link).  One pool per process, shared by
+// every context (Java keeps a context per thread; a multi-device batch runs
+// one thread per device): each copy() waits only for its own parts.
 class CopyPool {
  public:
   explicit CopyPool(int n) {
     for (int i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
-  }
-  ~CopyPool() {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    for (auto& t : th_) t.join();
   }
   int size() const { return (int)th_.size() + 1; }
   // memcpy split over the pool's threads and the caller; returns when done
@@ -84,48 +79,65 @@ class CopyPool {
       return;
     }
     const size_t per = ((bytes + parts - 1) / parts + 63) & ~size_t(63);
+    Group g;
     std::unique_lock<std::mutex> lk(mu_);
-    pending_ = 0;
     for (int i = 1; i < parts; ++i) {
       const size_t off = per * i;
       if (off >= bytes) break;
-      const size_t len = std::min(per, bytes - off);
-      ++pending_;
-      jobs_.push_back([=] { std::memcpy((char*)dst + off, (const char*)src + off, len); });
+      ++g.pending;
+      jobs_.push_back({&g, (char*)dst + off, (const char*)src + off, std::min(per, bytes - off)});
     }
     lk.unlock();
     cv_.notify_all();
     std::memcpy(dst, src, std::min(per, bytes));
     lk.lock();
-    done_.wait(lk, [this] { return pending_ == 0; });
+    done_.wait(lk, [&g] { return g.pending == 0; });
   }
 
  private:
+  struct Group {
+    int pending = 0;
+  };
+  struct Job {
+    Group* g;
+    char* d;
+    const char* s;
+    size_t n;
+  };
   void loop() {
     std::unique_lock<std::mutex> lk(mu_);
     for (;;) {
-      cv_.wait(lk, [this] { return stop_ || !jobs_.empty(); });
-      if (stop_) return;
-      auto job = std::move(jobs_.back());
-      jobs_.pop_back();
+      cv_.wait(lk, [this] { return !jobs_.empty(); });
+      const Job job = jobs_.front();
+      jobs_.pop_front();
       lk.unlock();
-      job();
+      std::memcpy(job.d, job.s, job.n);
       lk.lock();
-      if (--pending_ == 0) done_.notify_all();
+      if (--job.g->pending == 0) done_.notify_all();
     }
   }
   std::vector<std::thread> th_;
-  std::vector<std::function<void()>> jobs_;
+  std::deque<Job> jobs_;
   std::mutex mu_;
   std::condition_variable cv_, done_;
-  int pending_ = 0;
-  bool stop_ = false;
 };
+
+// The process's pool: its CPU share (sched affinity), at most 16 threads (the
+// GPU box's share per GPU), counting the caller.  Never destroyed (its
+// threads sleep until process exit).
+CopyPool& copy_pool() {
+  static CopyPool* pool = [] {
+    cpu_set_t cs;
+    int hw = (int)std::thread::hardware_concurrency();
+    if (sched_getaffinity(0, sizeof(cs), &cs) == 0) hw = CPU_COUNT(&cs);
+    return new CopyPool(std::max(0, std::min(hw, 16) - 1));
+  }();
+  return *pool;
+}
 
 struct PinRing {
   char* p[kPinSlots] = {};
   hipEvent_t ev[kPinSlots] = {};
-  CopyPool* pool = nullptr;
   double stat[6] = {};  // jwv_ctx_stage_stats
 };
 double now_s() {
@@ -162,12 +174,12 @@ struct jwv_ctx {
   struct Rec { int kind; double bytes; hipEvent_t e0, e1; };
   std::vector<Rec> recs;
   std::vector<hipEvent_t> ev_pool;
-  // overlapped 2-D schedule (body_2d_fwt): side streams for the resident
-  // passes, a ring of ordering events, per-column-group workspace pairs
-  hipStream_t side[2] = {nullptr, nullptr};
-  std::vector<hipEvent_t> xev;
-  size_t xev_next = 0;
-  std::vector<DevBuf> gws;
+};
+
+struct jwv_mctx {
+  std::vector<jwv_ctx*> ctx;  // one per listed device
+  std::string err;
+  std::mutex mu;
 };
 
 namespace {
@@ -417,11 +429,10 @@ int plan_of(jwv_ctx* c) { return c->plan >= 0 ? c->plan : ChainGeo::default_plan
 
 // A planned launch of an axis transform.  The planner turns the reference's
 // level loop into steps (tiled passes, the resident pass) before anything is
-// launched, so the overlapped 2-D schedule (body_2d_fwt) can run a plan's
-// resident pass on another stream while tiles of independent columns stream.
-// Every workspace a plan uses is allocated while it is built (grow()
-// synchronises the launch stream, which must not happen between the steps of
-// a schedule that forks other streams).
+// launched; every workspace a plan uses is allocated while it is built
+// (grow() synchronises the launch stream).  Round 5 measured a 2-D schedule
+// that ran the resident steps on side streams beside the tile passes of
+// independent column groups: slower, removed.
 struct Step {
   bool res = false;  // the resident pass (fwt_fwd_res / fwt_rev_res)
   int h = 0;         // res: forward input length / reverse output length
@@ -920,14 +931,9 @@ PinRing& pin_ring(jwv_ctx* c) {
   if (!r.p[0]) {
     for (int i = 0; i < kPinSlots; ++i) {
       hipchk(hipHostMalloc((void**)&r.p[i], kPinChunk, hipHostMallocDefault), "hipHostMalloc");
-      hipchk(hipEventCreateWithFlags(&r.ev[i], hipEventDisableTiming), "hipEventCreate");
+      if (!r.ev[i])
+        hipchk(hipEventCreateWithFlags(&r.ev[i], hipEventDisableTiming), "hipEventCreate");
     }
-    // copy threads: the process's CPU share (sched affinity), at most 16
-    // (the GPU box's share per GPU), counting the caller
-    cpu_set_t cs;
-    int hw = (int)std::thread::hardware_concurrency();
-    if (sched_getaffinity(0, sizeof(cs), &cs) == 0) hw = CPU_COUNT(&cs);
-    r.pool = new CopyPool(std::max(0, std::min(hw, 16) - 1));
   }
   return r;
 }
@@ -946,7 +952,7 @@ void copy_in(jwv_ctx* c, const double* x, double* dx, size_t n) {
     const double t0 = now_s();
     hipchk(hipEventSynchronize(r.ev[s]), "staging slot");  // its previous DMA is done
     const double t1 = now_s();
-    r.pool->copy(r.p[s], (const char*)x + off, len);
+    copy_pool().copy(r.p[s], (const char*)x + off, len);
     r.stat[1] += t1 - t0;
     r.stat[0] += now_s() - t1;
     hipchk(hipMemcpyAsync((char*)dx + off, r.p[s], len, hipMemcpyHostToDevice, c->stream), "H2D");
@@ -979,7 +985,7 @@ void copy_out(jwv_ctx* c, const double* dy, double* y, size_t n) {
     const double t0 = now_s();
     hipchk(hipEventSynchronize(r.ev[s]), "staging slot");
     const double t1 = now_s();
-    r.pool->copy((char*)y + off, r.p[s], len);
+    copy_pool().copy((char*)y + off, r.p[s], len);
     r.stat[2] += t1 - t0;
     r.stat[3] += now_s() - t1;
     if (k + kPinSlots < nk) issue(k + kPinSlots);
@@ -1019,173 +1025,12 @@ AxisFn axis_fn(Kind k, bool fwd) {
   return fwd ? wpt_fwd_axis : wpt_rev_axis;
 }
 
-// ---- overlapped 2-D FWT schedule
-// The resident passes (the latency-bound tails of each axis: one block per
-// row or column slab, a chain of levels with a barrier each) leave most of
-// the chip's HBM bandwidth idle.  They only touch part of the matrix, so
-// they can run beside the HBM-bound tile passes of the columns that do not
-// depend on them:
-//   forward  rows (tiles -> resident), then columns.  The row resident pass
-//            writes columns [0, hr) only; the column passes of [hr, cols) run
-//            beside it.  Each column group's resident pass runs on a side
-//            stream beside the next group's tiles.
-//   reverse  columns (resident -> tiles), then rows.  The row resident pass
-//            reads columns [0, hres) only: it runs beside the column tiles of
-//            [hres, cols) once group [0, hres) is done.  The column resident
-//            passes run ahead on a side stream.
-// Every column runs exactly the kernels of the serial schedule (its own
-// plan), so the result is bit-identical; only launch order and streams
-// differ.  Groups are multiples of 128 columns (whole XCD-paired slabs).
-#ifndef JWV_2D_OVERLAP
-#define JWV_2D_OVERLAP 1
-#endif
-#ifndef JWV_2D_GROUPS
-#define JWV_2D_GROUPS 4
-#endif
-#ifndef JWV_SIDE_PRIO
-#define JWV_SIDE_PRIO 1
-#endif
-constexpr int kOverlapMinElems = 1 << 22;
-constexpr int kColUnit = 128;
-constexpr size_t kEvRing = 64;
-
-hipStream_t side_stream(jwv_ctx* c, int i) {
-  if (!c->side[i]) {
-    int least = 0, greatest = 0;
-    HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    HIPCHK(hipStreamCreateWithPriority(&c->side[i], hipStreamNonBlocking,
-                                       JWV_SIDE_PRIO ? greatest : least));
-  }
-  return c->side[i];
-}
-// An ordering event recorded on s.  The ring is reused call after call: a
-// wait keeps the record it was enqueued against, so re-recording later is safe.
-hipEvent_t mark(jwv_ctx* c, hipStream_t s) {
-  hipEvent_t e;
-  if (c->xev.size() < kEvRing) {
-    hipchk(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
-    c->xev.push_back(e);
-  } else {
-    e = c->xev[c->xev_next++ % kEvRing];
-  }
-  hipchk(hipEventRecord(e, s), "hipEventRecord");
-  return e;
-}
-void wait_on(hipStream_t s, hipEvent_t e) { hipchk(hipStreamWaitEvent(s, e, 0), "hipStreamWaitEvent"); }
-// run f with s as the launch stream
-void on_stream(jwv_ctx* c, hipStream_t s, const std::function<void()>& f) {
-  hipStream_t keep = c->stream;
-  c->stream = s;
-  try {
-    f();
-  } catch (...) {
-    c->stream = keep;
-    throw;
-  }
-  c->stream = keep;
-}
-
-struct ColGroup {
-  int c0, w;
-  Plan p;
-};
-// [lo, hi) as up to n groups of whole kColUnit-column units
-void split_cols(std::vector<ColGroup>& out, int lo, int hi, int n) {
-  const int units = (hi - lo) / kColUnit;
-  n = std::max(1, std::min(n, units));
-  for (int i = 0; i < n; ++i) {
-    const int a = lo + (int)((int64_t)units * i / n) * kColUnit;
-    const int e = i + 1 == n ? hi : lo + (int)((int64_t)units * (i + 1) / n) * kColUnit;
-    out.push_back({a, e - a, {}});
-  }
-}
-
-bool body_2d_fwt(jwv_ctx* c, bool fwd, const Bank& b, const double* x, double* y, double* tmp,
-                 int64_t rows, int64_t cols, int lvl_m, int lvl_n) {
-  if (!JWV_2D_OVERLAP || rows * cols < kOverlapMinElems || cols % kColUnit) return false;
-  const AxisView rv = cview(cols, 1), cvw = cview(rows, cols);
-  // plans first (they allocate), launches after
-  Plan R = fwd ? fwt_fwd_plan(c, b, Axis{x, rv, tmp, rv, rows, (int)cols, 1}, lvl_n, c->ws)
-               : fwt_rev_plan(c, b, Axis{tmp, rv, y, rv, rows, (int)cols, 1}, lvl_n, c->ws);
-  const Step* rres = nullptr;
-  if (!R.empty() && (fwd ? R.back().res : R.front().res)) rres = fwd ? &R.back() : &R.front();
-  const int hr = rres ? rres->h : 0;  // columns the row resident pass touches
-  if (hr % kColUnit || hr >= cols) return false;
-  std::vector<ColGroup> g;
-  if (hr) g.push_back({0, hr, {}});
-  split_cols(g, hr, (int)cols, JWV_2D_GROUPS);
-  if (c->gws.size() < 2 * g.size()) c->gws.resize(2 * g.size());
-  for (size_t i = 0; i < g.size(); ++i) {
-    const double* src = fwd ? tmp + g[i].c0 : x + g[i].c0;
-    double* dst = fwd ? y + g[i].c0 : tmp + g[i].c0;
-    const Axis a{src, cvw, dst, cvw, 1, (int)rows, g[i].w};
-    g[i].p = fwd ? fwt_fwd_plan(c, b, a, lvl_m, &c->gws[2 * i])
-                 : fwt_rev_plan(c, b, a, lvl_m, &c->gws[2 * i]);
-  }
-  hipStream_t s0 = c->stream, s1 = side_stream(c, 0), s2 = side_stream(c, 1);
-  if (fwd) {
-    for (const Step& s : R)
-      if (&s != rres) s.go();
-    hipEvent_t er = nullptr;
-    if (rres) {
-      wait_on(s2, mark(c, s0));
-      on_stream(c, s2, rres->go);
-      er = mark(c, s2);
-    }
-    // group order: the first independent group, then [0, hr) (its row
-    // resident pass has had one group's time to finish), then the rest
-    std::vector<size_t> order;
-    for (size_t i = hr ? 1 : 0; i < g.size(); ++i) {
-      order.push_back(i);
-      if (hr && i == 1) order.push_back(0);
-    }
-    if (hr && g.size() == 1) order.push_back(0);
-    for (size_t i : order) {
-      if (hr && i == 0) wait_on(s0, er);
-      const Plan& p = g[i].p;
-      const bool tail = p.back().res;
-      for (size_t k = 0; k + (tail ? 1 : 0) < p.size(); ++k) p[k].go();
-      if (tail) {
-        wait_on(s1, mark(c, s0));
-        on_stream(c, s1, p.back().go);
-      }
-    }
-    wait_on(s0, mark(c, s1));
-    if (er) wait_on(s0, er);
-  } else {
-    wait_on(s1, mark(c, s0));
-    std::vector<hipEvent_t> ea(g.size(), nullptr);
-    for (size_t i = 0; i < g.size(); ++i)
-      if (g[i].p.front().res) {
-        on_stream(c, s1, g[i].p.front().go);
-        ea[i] = mark(c, s1);
-      }
-    hipEvent_t er = nullptr;
-    for (size_t i = 0; i < g.size(); ++i) {
-      const Plan& p = g[i].p;
-      if (ea[i]) wait_on(s0, ea[i]);
-      for (size_t k = ea[i] ? 1 : 0; k < p.size(); ++k) p[k].go();
-      if (hr && i == 0) {
-        wait_on(s2, mark(c, s0));
-        on_stream(c, s2, rres->go);
-        er = mark(c, s2);
-      }
-    }
-    wait_on(s0, mark(c, s1));
-    if (er) wait_on(s0, er);
-    for (const Step& s : R)
-      if (&s != rres) s.go();
-  }
-  return true;
-}
-
 // BasicTransform.java:361-399 (forward: rows lvlN -> columns lvlM) and
 // :436-474 (reverse: columns lvlM -> rows lvlN).
 void body_2d(jwv_ctx* c, Kind k, bool fwd, const Bank& b, const double* x, double* y,
              int64_t rows, int64_t cols, int lvl_m, int lvl_n) {
   if (rows == 0 || cols == 0) return;
   double* tmp = grow(c, c->big, (size_t)(rows * cols));
-  if (k == Kind::FWT && body_2d_fwt(c, fwd, b, x, y, tmp, rows, cols, lvl_m, lvl_n)) return;
   const AxisView rv = cview(cols, 1), cvw = cview(rows, cols);
   AxisFn f = axis_fn(k, fwd);
   if (fwd) {
@@ -1600,16 +1445,10 @@ int jwv_ctx_destroy(jwv_ctx* c) {
   if (c->sync) hipFree(c->sync);
   for (auto& r : c->recs) { hipEventDestroy(r.e0); hipEventDestroy(r.e1); }
   for (auto e : c->ev_pool) hipEventDestroy(e);
-  for (auto e : c->xev) hipEventDestroy(e);
-  for (DevBuf& b : c->gws)
-    if (b.p) hipFree(b.p);
-  for (hipStream_t s : c->side)
-    if (s) hipStreamDestroy(s);
   for (int i = 0; i < kPinSlots; ++i) {
     if (c->pin.p[i]) hipHostFree(c->pin.p[i]);
     if (c->pin.ev[i]) hipEventDestroy(c->pin.ev[i]);
   }
-  delete c->pin.pool;
   if (c->own) hipStreamDestroy(c->own);
   delete c;
   if (prev >= 0) hipSetDevice(prev);
@@ -1717,9 +1556,11 @@ int jwv_ctx_trim(jwv_ctx* c) {
       b->p = nullptr;
       b->n = 0;
     }
-    for (DevBuf& g : c->gws)
-      if (g.p) hipchk(hipFree(g.p), "free");
-    c->gws.clear();
+    for (int i = 0; i < kPinSlots; ++i)
+      if (c->pin.p[i]) {
+        hipchk(hipHostFree(c->pin.p[i]), "hipHostFree");
+        c->pin.p[i] = nullptr;
+      }
   });
 }
 
@@ -2127,5 +1968,112 @@ int jwv_modwt_inv_ld_f64_dev(const double* wv, int64_t ldw, double* x, int64_t n
     body_modwt_inv(c, b, wv, x, n, J, ldw);
   });
 }
+
+// ---- multi-device batches ----------------------------------------------------
+int jwv_batch_split(int64_t batch, int n, int i, int64_t* start, int64_t* count) {
+  if (batch < 0 || n < 1 || i < 0 || i >= n || !start || !count)
+    return set_err(nullptr, JWV_ERR_BAD_CALL, "jwv_batch_split: bad arguments");
+  // floor(batch * k / n) without overflow: (batch / n) * k + (batch % n) * k / n
+  auto at = [&](int64_t k) { return (batch / n) * k + (batch % n) * k / n; };
+  *start = at(i);
+  *count = at(i + 1) - *start;
+  return JWV_OK;
+}
+
+int jwv_mctx_create(const int* devices, int n, jwv_mctx** out) {
+  if (!out) return set_err(nullptr, JWV_ERR_BAD_CALL, "out is NULL");
+  *out = nullptr;
+  if (!devices || n < 1) return set_err(nullptr, JWV_ERR_BAD_CALL, "no devices given");
+  jwv_mctx* m = new jwv_mctx();
+  for (int i = 0; i < n; ++i) {
+    jwv_ctx* c = nullptr;
+    const int rc = jwv_ctx_create(devices[i], &c);
+    if (rc != JWV_OK) {
+      const std::string why = g_tls_error;
+      jwv_mctx_destroy(m);
+      return set_err(nullptr, rc, "device " + std::to_string(devices[i]) + ": " + why);
+    }
+    m->ctx.push_back(c);
+  }
+  *out = m;
+  return JWV_OK;
+}
+
+int jwv_mctx_destroy(jwv_mctx* m) {
+  if (!m) return JWV_OK;
+  for (jwv_ctx* c : m->ctx) jwv_ctx_destroy(c);
+  delete m;
+  return JWV_OK;
+}
+
+const char* jwv_mctx_last_error(const jwv_mctx* m) {
+  return m ? m->err.c_str() : g_tls_error.c_str();
+}
+
+int jwv_mctx_size(const jwv_mctx* m) { return m ? (int)m->ctx.size() : 0; }
+
+jwv_ctx* jwv_mctx_ctx(jwv_mctx* m, int i) {
+  return (m && i >= 0 && i < (int)m->ctx.size()) ? m->ctx[i] : nullptr;
+}
+
+int jwv_mctx_set_math(jwv_mctx* m, int mode) {
+  if (!m) return set_err(nullptr, JWV_ERR_BAD_CALL, "jwv_mctx is NULL");
+  for (jwv_ctx* c : m->ctx) {
+    const int rc = jwv_ctx_set_math(c, mode);
+    if (rc != JWV_OK) {
+      m->err = jwv_last_error(c);
+      return rc;
+    }
+  }
+  return JWV_OK;
+}
+
+namespace {
+using BatchFn = int (*)(const double*, double*, int64_t, int64_t, int64_t, int, const jwv_taps*,
+                        jwv_ctx*);
+int mbatch(Kind k, bool fwd, BatchFn fn, const double* x, double* y, int64_t batch, int64_t n,
+           int64_t ld, int level, const jwv_taps* t, jwv_mctx* m) {
+  if (!m) return set_err(nullptr, JWV_ERR_BAD_CALL, "jwv_mctx is NULL");
+  std::lock_guard<std::mutex> lk(m->mu);
+  m->err.clear();
+  try {  // once, with the single-device entries' checks and messages
+    (void)make_bank(t);
+    if (batch < 0 || ld < n) throw Fail{JWV_ERR_BAD_CALL, "batch < 0 or ld < n"};
+    check_1d(k, fwd, n, level);
+    if (batch == 0) return JWV_OK;
+    check_ptrs(x, y);
+  } catch (const Fail& e) {
+    m->err = e.msg;
+    return e.code;
+  }
+  const int D = (int)m->ctx.size();
+  std::vector<int> rc(D, JWV_OK);
+  auto work = [&](int i) {
+    int64_t s0 = 0, cnt = 0;
+    jwv_batch_split(batch, D, i, &s0, &cnt);
+    if (cnt > 0) rc[i] = fn(x + s0 * ld, y + s0 * ld, cnt, n, ld, level, t, m->ctx[i]);
+  };
+  std::vector<std::thread> th;
+  for (int i = 1; i < D; ++i) th.emplace_back(work, i);
+  work(0);
+  for (auto& h : th) h.join();
+  for (int i = 0; i < D; ++i)
+    if (rc[i] != JWV_OK) {
+      m->err = "device " + std::to_string(m->ctx[i]->device) + ": " + jwv_last_error(m->ctx[i]);
+      return rc[i];
+    }
+  return JWV_OK;
+}
+}  // namespace
+
+#define JWV_MBATCH(NAME, SINGLE, KIND, FWD)                                                    \
+  int NAME(const double* x, double* y, int64_t batch, int64_t n, int64_t ld, int level,         \
+           const jwv_taps* t, jwv_mctx* m) {                                                    \
+    return mbatch(KIND, FWD, SINGLE, x, y, batch, n, ld, level, t, m);                          \
+  }
+JWV_MBATCH(jwv_m_fwt_fwd_batch_f64, jwv_fwt_fwd_batch_f64, Kind::FWT, true)
+JWV_MBATCH(jwv_m_fwt_rev_batch_f64, jwv_fwt_rev_batch_f64, Kind::FWT, false)
+JWV_MBATCH(jwv_m_wpt_fwd_batch_f64, jwv_wpt_fwd_batch_f64, Kind::WPT, true)
+JWV_MBATCH(jwv_m_wpt_rev_batch_f64, jwv_wpt_rev_batch_f64, Kind::WPT, false)
 
 }  // extern "C"

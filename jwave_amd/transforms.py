@@ -125,6 +125,76 @@ class Context:
         raise JWaveError(msg)
 
 
+def _raise_for(rc, msg):
+    if rc == L.JWV_ERR_FAILURE:
+        raise JWaveFailure(msg)
+    if rc == L.JWV_ERR_ILLEGAL_ARGUMENT:
+        raise ValueError(msg)  # IllegalArgumentException
+    raise JWaveError(msg)
+
+
+def batch_split(batch, n_devices, i):
+    """(start, count) of device i's contiguous block of a batch spread over
+    n_devices (jwv_batch_split: start = floor(batch*i/n))."""
+    lib = L.lib()
+    s, c = ctypes.c_int64(0), ctypes.c_int64(0)
+    rc = lib.jwv_batch_split(int(batch), int(n_devices), int(i), ctypes.byref(s), ctypes.byref(c))
+    if rc != 0:
+        _raise_for(rc, (lib.jwv_last_error(None) or b"").decode())
+    return s.value, c.value
+
+
+class MultiContext:
+    """A jwv_mctx: one context per listed device.  Batched host arrays are
+    split into contiguous blocks of signals, one per device, transformed
+    concurrently (each device over its own PCIe link, no collective) and
+    returned as one array -- the executor-over-signals batch of
+    src/test/java/jwave/ParallelizationOpportunityTest.java:80-98 over the
+    node's GPUs.  Results equal the single-device batched call."""
+
+    def __init__(self, devices=(0,), math="exact"):
+        self._lib = L.lib()
+        devs = [int(d) for d in devices]
+        arr = (ctypes.c_int * len(devs))(*devs)
+        h = ctypes.c_void_p()
+        rc = self._lib.jwv_mctx_create(arr, len(devs), ctypes.byref(h))
+        if rc != 0:
+            _raise_for(rc, (self._lib.jwv_mctx_last_error(None) or b"").decode())
+        self.handle = h
+        self.devices = devs
+        mode = {"exact": L.JWV_MATH_EXACT, "fma": L.JWV_MATH_FMA}[math]
+        self._check(self._lib.jwv_mctx_set_math(self.handle, mode))
+        self.math = math
+
+    def _check(self, rc):
+        if rc != 0:
+            _raise_for(rc, (self._lib.jwv_mctx_last_error(self.handle) or b"").decode())
+
+    def batch(self, x, wavelet, level, forward=True, kind="fwt"):
+        """Every row of the host array x (batch x n) transformed with `level`."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        if x.ndim != 2:
+            raise JWaveFailure("MultiContext.batch: a 2-D array of signals is required")
+        b, n = x.shape
+        y = np.empty_like(x)
+        name = "jwv_m_%s_%s_batch_f64" % (kind, "fwd" if forward else "rev")
+        t = _TapsHolder.of(wavelet)
+        self._check(getattr(self._lib, name)(x.ctypes.data, y.ctypes.data, b, n, n, int(level),
+                                             t, self.handle))
+        return y
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self._lib.jwv_mctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 _tls = threading.local()
 
 
@@ -550,17 +620,22 @@ class WaveletTransform(BasicTransform):
         self._check_1d(n, level, False)
         return fwt_reverse(arr, self._wavelet, level, self._ctx, self.kind)
 
-    def forward_batch(self, signals, level=None):
-        """Batched 1-D forward: one row per independent signal (one native call)."""
+    def forward_batch(self, signals, level=None, mctx=None):
+        """Batched 1-D forward: one row per independent signal (one native
+        call; with a MultiContext, host rows split over its devices)."""
         n = signals.shape[1]
         level = get_exponent(n) if level is None else level
         self._check_1d(n, level, True)
+        if mctx is not None:
+            return mctx.batch(signals, self._wavelet, level, True, self.kind)
         return fwt_forward(signals, self._wavelet, level, self._ctx, self.kind)
 
-    def reverse_batch(self, coeffs, level=None):
+    def reverse_batch(self, coeffs, level=None, mctx=None):
         n = coeffs.shape[1]
         level = get_exponent(n) if level is None else level
         self._check_1d(n, level, False)
+        if mctx is not None:
+            return mctx.batch(coeffs, self._wavelet, level, False, self.kind)
         return fwt_reverse(coeffs, self._wavelet, level, self._ctx, self.kind)
 
     # WaveletTransform.decompose / recompose (:136-182)
@@ -603,6 +678,31 @@ class FastWaveletTransform(WaveletTransform):
             raise JWaveFailure(who + _BINARY_MSG)
         if level < 0 or level > get_exponent(n):  # :80-83 / :128-131
             raise JWaveFailure(who + "given level is out of range for given array")
+
+
+class InPlaceFastWaveletTransform(FastWaveletTransform):
+    """InPlaceFastWaveletTransform.java:33-121: forwardInPlace / reverseInPlace
+    overwrite the caller's array (numpy array or torch tensor) with the result
+    and return that same object.  Each is one native call; the array is
+    written only after the call succeeded, so a failing call leaves it as it
+    was (the reference copies back after super.forward returned).  forward /
+    reverse stay out of place (:106-121)."""
+
+    @staticmethod
+    def _store(arr, out):
+        if _is_torch(arr):
+            arr.copy_(out)
+        else:
+            arr[...] = out
+        return arr
+
+    def forwardInPlace(self, arrTime, level=None):  # noqa: N802,N803 (reference names)
+        # forwardInPlace(a) = super.forward(a): WaveletTransform.forward(double[])
+        # (:77-88) checks the length with its own message, then maximal level
+        return self._store(arrTime, self.forward_1d(arrTime, level))
+
+    def reverseInPlace(self, arrHilb, level=None):  # noqa: N802,N803
+        return self._store(arrHilb, self.reverse_1d(arrHilb, level))
 
 
 class WaveletPacketTransform(WaveletTransform):
@@ -847,7 +947,9 @@ class ParallelTransform(BasicTransform):
         self._transform = transform
         self._parallelism = parallelism
         self.kind = transform.kind
-        self._name = transform.getName()
+        # ParallelTransform never sets _name: getName() is null
+        # (BasicTransform.java:56-58, 69-71)
+        self._name = None
 
     def _check_1d(self, n, level, fwd):
         return self._transform._check_1d(n, level, fwd)
@@ -859,10 +961,18 @@ class ParallelTransform(BasicTransform):
         return self._transform.reverse_1d(arr, *levels)
 
     def _par(self, what, fn, *args):
+        # The reference's tasks wrap the JWaveException in a RuntimeException
+        # (ParallelTransform.java:259-269), whose message is the cause's
+        # Throwable.toString(): "jwave.exceptions.JWaveFailure: <msg>".  When
+        # the failing task ran on a pool worker, ForkJoinTask may re-wrap it
+        # once more ("java.lang.RuntimeException: ..."); which task fails first
+        # is scheduling-dependent, so that extra prefix is not reproduced
+        # (parity unpinned, tests/test_parallel_transform.py).
         try:
             return fn(*args)
         except JWaveException as e:
-            raise JWaveException("Error in parallel %s transform: %s" % (what, e.getMessage()))
+            raise JWaveException("Error in parallel %s transform: jwave.exceptions.%s: %s"
+                                 % (what, type(e).__name__, e.getMessage()))
 
     def forward_2d(self, m, lvl_m=None, lvl_n=None):
         r, c = m.shape

@@ -148,3 +148,29 @@ int jwv_decompose_f64(const double* x, double* mat, int64_t n, int tr, const jwv
   while (((int64_t)1 << lg) < n) ++lg;
   return rec("jwv_decompose_f64", x, n, mat, (lg + 1) * n, 21, t, n, tr, 0, 0, 0, 0);
 }
+
+/* multi-device context: records the device list; batches go through rec()
+ * with k = 30..33 and the device count in a[4] */
+struct jwv_mctx { int n; int dev[16]; };
+static struct jwv_mctx g_mctx;
+int fc_mctx_devices(int* out) {
+  for (int i = 0; i < g_mctx.n; ++i) out[i] = g_mctx.dev[i];
+  return g_mctx.n;
+}
+int jwv_mctx_create(const int* devices, int n, jwv_mctx** out) {
+  g_mctx.n = n < 16 ? n : 16;
+  for (int i = 0; i < g_mctx.n; ++i) g_mctx.dev[i] = devices[i];
+  *out = &g_mctx;
+  return JWV_OK;
+}
+const char* jwv_mctx_last_error(const jwv_mctx* m) { return "fake multi error text"; }
+jwv_ctx* jwv_mctx_ctx(jwv_mctx* m, int i) { return (m && i >= 0 && i < m->n) ? &g_ctx : NULL; }
+#define TM(NAME, K)                                                                   \
+  int NAME(const double* x, double* y, int64_t b, int64_t n, int64_t ld, int lv,     \
+           const jwv_taps* t, jwv_mctx* m) {                                         \
+    return rec(#NAME, x, b * ld, y, b * ld, K, t, b, n, ld, lv, m->n, 0);            \
+  }
+TM(jwv_m_fwt_fwd_batch_f64, 30)
+TM(jwv_m_fwt_rev_batch_f64, 31)
+TM(jwv_m_wpt_fwd_batch_f64, 32)
+TM(jwv_m_wpt_rev_batch_f64, 33)

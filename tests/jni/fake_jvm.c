@@ -13,7 +13,7 @@
 #include <string.h>
 
 struct fake_jobject {
-  int kind; /* 1 double[], 2 long[], 3 String, 4 Class */
+  int kind; /* 1 double[], 2 long[], 3 String, 4 Class, 5 int[] */
   jsize len;
   void* data;
   char name[128];
@@ -53,6 +53,9 @@ static void SetDoubleArrayRegion(JNIEnv* env, jdoubleArray a, jsize s, jsize n, 
 static void SetLongArrayRegion(JNIEnv* env, jlongArray a, jsize s, jsize n, const jlong* b) {
   if (region_ok(a, 2, s, n)) memcpy((jlong*)a->data + s, b, (size_t)n * sizeof(jlong));
 }
+static void GetIntArrayRegion(JNIEnv* env, jintArray a, jsize s, jsize n, jint* b) {
+  if (region_ok(a, 5, s, n)) memcpy(b, (jint*)a->data + s, (size_t)n * sizeof(jint));
+}
 static jboolean ExceptionCheck(JNIEnv* env) { return t_exc[0] != 0; }
 static jstring NewStringUTF(JNIEnv* env, const char* s) {
   struct fake_jobject* o = calloc(1, sizeof *o);
@@ -73,7 +76,8 @@ static jint ThrowNew(JNIEnv* env, jclass cls, const char* msg) {
 
 static const struct JNINativeInterface_ g_table = {
     GetArrayLength, GetDoubleArrayRegion, SetDoubleArrayRegion, SetLongArrayRegion,
-    ExceptionCheck, NewStringUTF,         FindClass,            ThrowNew};
+    GetIntArrayRegion, ExceptionCheck,    NewStringUTF,         FindClass,
+    ThrowNew};
 static const struct JNINativeInterface_* g_env = &g_table;
 
 /* ---- helpers for the Python tests */
@@ -91,6 +95,14 @@ jlongArray fj_larray(jsize n) {
   o->kind = 2;
   o->len = n;
   o->data = calloc(n > 0 ? (size_t)n : 1, sizeof(jlong));
+  return o;
+}
+jintArray fj_iarray(jsize n, const jint* init) {
+  struct fake_jobject* o = calloc(1, sizeof *o);
+  o->kind = 5;
+  o->len = n;
+  o->data = calloc(n > 0 ? (size_t)n : 1, sizeof(jint));
+  if (init) memcpy(o->data, init, (size_t)n * sizeof(jint));
   return o;
 }
 void* fj_data(jarray a) { return a->data; }

@@ -1,7 +1,7 @@
 /*
  * jni.h — TEST DOUBLE, not a JDK header.  The development image has no JDK,
  * so the JNI shim (java/native/jwave_hip_jni.c) is compiled for its CPU tests
- * against this minimal stand-in: the JNI types and the eight JNIEnv functions
+ * against this minimal stand-in: the JNI types and the nine JNIEnv functions
  * the shim calls, with the real JNI calling shape ((*env)->Fn(env, ...)).
  * The function table is filled by tests/jni/fake_jvm.c, which models Java
  * arrays and the pending-exception state (ArrayIndexOutOfBounds on a bad
@@ -30,6 +30,7 @@ typedef jobject jthrowable;
 typedef jobject jarray;
 typedef jarray jdoubleArray;
 typedef jarray jlongArray;
+typedef jarray jintArray;
 
 struct JNINativeInterface_;
 typedef const struct JNINativeInterface_* JNIEnv;
@@ -40,6 +41,7 @@ struct JNINativeInterface_ {
   void (*SetDoubleArrayRegion)(JNIEnv* env, jdoubleArray a, jsize start, jsize len,
                                const jdouble* buf);
   void (*SetLongArrayRegion)(JNIEnv* env, jlongArray a, jsize start, jsize len, const jlong* buf);
+  void (*GetIntArrayRegion)(JNIEnv* env, jintArray a, jsize start, jsize len, jint* buf);
   jboolean (*ExceptionCheck)(JNIEnv* env);
   jstring (*NewStringUTF)(JNIEnv* env, const char* s);
   jclass (*FindClass)(JNIEnv* env, const char* name);

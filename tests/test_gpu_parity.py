@@ -567,6 +567,41 @@ def test_facade_and_classes(ctx):
     assert jw.Transform(jw.FastWaveletTransform(jw.by_class("Haar1"), ctx)).forward(np.ones(3)) is None
 
 
+def test_in_place_fwt(ctx):
+    """InPlaceFastWaveletTransform (InPlaceFastWaveletTransform.java:70-120):
+    forwardInPlace / reverseInPlace return the caller's own array holding the
+    result, bit-identical to the oracle, for numpy arrays and device tensors,
+    at the maximal and a given level; a failing call (level out of range,
+    non-power-of-two length) raises the reference's message and leaves the
+    array untouched; forward / reverse stay out of place."""
+    import torch
+    w = jw.by_class("Daubechies4")
+    t = jw.InPlaceFastWaveletTransform(w, ctx)
+    for n, lev in ((1 << 14, None), (1 << 14, 5), (1 << 20, None), (2, None)):
+        x = rnd(n, n + 1)
+        full = n.bit_length() - 1 if lev is None else lev
+        yr = oracle.fwt_forward(w, x, full)
+        a = x.copy()
+        assert t.forwardInPlace(a, lev) is a
+        assert_exact(a, yr, "in-place fwd n=%d" % n)
+        assert t.reverseInPlace(a, lev) is a
+        assert_exact(a, oracle.fwt_reverse(w, yr, full), "in-place rev n=%d" % n)
+        d = torch.from_numpy(x.copy()).cuda()
+        assert t.forwardInPlace(d, lev) is d
+        torch.cuda.synchronize()
+        assert_exact(d.cpu().numpy(), yr, "in-place fwd tensor n=%d" % n)
+    x = rnd(1024, 5)
+    a = x.copy()
+    with pytest.raises(jw.JWaveFailure, match="^FastWaveletTransform#forward - given level is out"):
+        t.forwardInPlace(a, 11)
+    assert np.array_equal(a, x)
+    with pytest.raises(jw.JWaveFailure, match="^WaveletTransform#reverse - given array length"):
+        t.reverseInPlace(np.ones(12))
+    y = t.forward(x)
+    assert y is not x and np.array_equal(x, rnd(1024, 5))
+    assert_exact(y, oracle.fwt_forward(w, x, 10), "out-of-place forward")
+
+
 @pytest.mark.parametrize("kind,wname,R,cw,lev", [
     ("fwt", "Daubechies4", 1024, 24, 10), ("fwt", "Symlet8", 16384, 8, 14),
     ("fwt", "Haar1", 64, 3, 6), ("fwt", "Daubechies8", 32768, 16, 7),

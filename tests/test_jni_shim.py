@@ -78,9 +78,16 @@ def _declare(lib):
     lib.Java_jwave_amd_HipNative_modwt.argtypes = [P, P, J, B, P, P, I, I, I, I, P, P, P, P]
     lib.Java_jwave_amd_HipNative_aed.argtypes = [P, P, J, I, B, P, P] + taps
     lib.Java_jwave_amd_HipNative_decompose.argtypes = [P, P, J, I, P, P] + taps
+    lib.fj_iarray.restype = P
+    lib.fj_iarray.argtypes = [I, P]
+    lib.Java_jwave_amd_HipNative_mctxCreate.argtypes = [P, P, P, P]
+    lib.Java_jwave_amd_HipNative_mctxLastError.argtypes = [P, P, J]
+    lib.Java_jwave_amd_HipNative_mctxLastError.restype = P
+    lib.Java_jwave_amd_HipNative_transformBatchMulti.argtypes = ([P, P, J, I, B, P, P, I, I, I]
+                                                                 + taps)
     for f in ("transform1d", "transformBatch", "transform2d", "transform3d", "transform3dPt",
               "modwt", "aed",
-              "decompose", "ctxCreate"):
+              "decompose", "ctxCreate", "mctxCreate", "transformBatchMulti"):
         getattr(lib, "Java_jwave_amd_HipNative_" + f).restype = I
     return lib
 
@@ -275,6 +282,67 @@ def test_status_passthrough_leaves_output_untouched(jvm):
     jvm.lib.fc_set_rc(0)
     msg = jvm.lib.fj_string(jvm.native("lastError", ctx))
     assert msg == b"fake error text"
+
+
+def test_in_place_same_array(jvm):
+    """HipInPlaceFastWaveletTransform.forwardInPlace / reverseInPlace pass the
+    caller's array as both input and output (InPlaceFastWaveletTransform.java:70-120):
+    the shim stages the input before the call, so the result lands in that
+    array; a failing call leaves it untouched (the reference copies back only
+    after super.forward returned)."""
+    w = _w("Daubechies4")
+    ctx = _ctx(jvm)
+    x = np.linspace(-1.0, 1.0, 512)
+    ja = jvm.darray(x)
+    assert jvm.native("transform1d", ctx, 0, 1, ja, ja, 9, *jvm.taps(w)) == 0
+    c = jvm.last()
+    assert c.name == b"jwv_fwt_fwd_f64" and c.a[0] == 512 and c.a[1] == 9
+    assert np.array_equal(jvm.read(ja, 512), 2 * x + 1)
+    assert jvm.native("transform1d", ctx, 0, 0, ja, ja, 9, *jvm.taps(w)) == 0
+    assert np.array_equal(jvm.read(ja, 512), 2 * (2 * x + 1) + 2)
+    before = jvm.read(ja, 512)
+    jvm.lib.fc_set_rc(1)
+    assert jvm.native("transform1d", ctx, 0, 1, ja, ja, 20, *jvm.taps(w)) == 1
+    jvm.lib.fc_set_rc(0)
+    assert np.array_equal(jvm.read(ja, 512), before)
+
+
+def test_multi_device_batch_marshaling(jvm):
+    """HipWaveletPacketTransform.forwardBatch under -Djwave.hip.devices=0,1,2
+    (HipNative.mctx): mctxCreate passes the device list, transformBatchMulti
+    stages the packed batch once and calls the multi-device entry with the
+    batch geometry; its status passes through and a failure leaves the output
+    untouched."""
+    jvm.lib.fc_mctx_devices.argtypes = [P]
+    devs = (ctypes.c_int32 * 3)(0, 1, 2)
+    jd = jvm.lib.fj_iarray(3, ctypes.cast(devs, P))
+    h = jvm.lib.fj_larray(1)
+    assert jvm.native("mctxCreate", jd, h) == 0
+    m = ctypes.cast(jvm.lib.fj_data(h), ctypes.POINTER(ctypes.c_int64))[0]
+    got = (ctypes.c_int32 * 16)()
+    assert jvm.lib.fc_mctx_devices(ctypes.cast(got, P)) == 3 and list(got[:3]) == [0, 1, 2]
+    w = _w("Symlet8")
+    x = np.arange(6 * 256, dtype=np.float64)
+    for kind, fwd, name, k in [(0, 1, b"jwv_m_fwt_fwd_batch_f64", 30),
+                               (0, 0, b"jwv_m_fwt_rev_batch_f64", 31),
+                               (1, 1, b"jwv_m_wpt_fwd_batch_f64", 32),
+                               (1, 0, b"jwv_m_wpt_rev_batch_f64", 33)]:
+        jx, jy = jvm.darray(x), jvm.empty(x.size)
+        assert jvm.native("transformBatchMulti", m, kind, fwd, jx, jy, 6, 256, 5,
+                          *jvm.taps(w)) == 0
+        c = jvm.last()
+        assert c.name == name and list(c.a[:5]) == [6, 256, 256, 5, 3]
+        assert np.array_equal(jvm.read(jy, x.size), 2 * x + k)
+    jy = jvm.empty(x.size)
+    jvm.lib.fc_set_rc(3)
+    assert jvm.native("transformBatchMulti", m, 1, 1, jvm.darray(x), jy, 6, 256, 5,
+                      *jvm.taps(w)) == 3
+    jvm.lib.fc_set_rc(0)
+    assert not jvm.read(jy, x.size).any()
+    msg = jvm.native("mctxLastError", m)
+    assert jvm.lib.fj_string(msg) == b"fake multi error text"
+    jvm.lib.fj_free(jd)
+    jvm.lib.fj_free(h)
 
 
 def test_staging_per_thread_reuse_and_cap(jvm):
