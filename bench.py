@@ -654,21 +654,18 @@ def host_entry(args, d, reps=5):
     return out
 
 
-def main():
-    args = parse()
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(launch_ranks(args))
-    d = Dist(args.gpus, args.dry_run)
-    W = setup_dry(args, d) if args.dry_run else setup(args, d)
+def measure(args, d, W, workload, steps, warmup, math):
+    """Warmup (W steps, then at least --warmup-seconds), timed region A
+    (the metric, no events), timed region B (every launch evented in its own
+    dispatch packet) -> the dominant kind's roofline."""
     step, ctx = W["step"], W["ctx"]
-
     # W warmup steps, and at least --warmup-seconds of them: MI355X needs
     # ~10 ms of sustained work before its step time settles (config 2, one
     # box: 110-123 us/step over the first 60 steps, 106 us after), so a short
     # W would time the ramp, not the kernels.  The line reports both counts.
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
-    wsteps = args.warmup
+    wsteps = warmup
     d.sync()
     t0 = time.perf_counter()
     # chunks of 16 steps; every rank takes the same decision (the sharded
@@ -685,9 +682,9 @@ def main():
     # check runs after the timed regions, on the same step's outputs.
     # timed region A: the metric (no events)
     issue = []
-    el = d.max(timed(d, step, args.steps, issue))
-
-    out_roof, out_fp64, tb = None, None, None
+    el = d.max(timed(d, step, steps, issue))
+    r = {"el": el, "issue": issue[0], "wsteps": wsteps, "prof": {}, "tb": None, "roof": None,
+         "fp64": None}
     if ctx is not None:
         # timed region B: same steps, every launch carrying start/stop events
         # in its own dispatch packet (hipExtLaunchKernelGGL: the kernel's
@@ -696,31 +693,83 @@ def main():
         # longer than rocprofv3 (config 2 / 5, r04m).
         ctx.profile_select(None)
         ctx.profile(True)
-        tb = d.max(timed(d, step, args.steps))
+        r["tb"] = d.max(timed(d, step, steps))
         ctx.profile(False)
-        prof = ctx.profile_read()
+        prof = r["prof"] = ctx.profile_read()
         kname = max(prof.items(), key=lambda kv: kv[1]["total_ms"])[0]
         ks = prof[kname]
         avg_ms = ks["total_ms"] / ks["launches"]
         bytes_per_launch = ks["bytes"] / ks["launches"]
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-        traffic, tsrc = load_traffic(args.workload, kname, args.math)
-        out_roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                    "kernel": kname, "avg_launch_us": round(avg_ms * 1e3, 2),
-                    "algorithmic_bytes_per_launch": bytes_per_launch, "launches": ks["launches"]}
+        traffic, tsrc = load_traffic(workload, kname, math)
+        r["roof"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                     "kernel": kname, "avg_launch_us": round(avg_ms * 1e3, 2),
+                     "algorithmic_bytes_per_launch": bytes_per_launch, "launches": ks["launches"]}
         if tsrc:
-            out_roof["traffic_source"] = tsrc
+            r["roof"]["traffic_source"] = tsrc
         if W.get("flops_per_sample"):
             # second bound: algorithmic FP64 flops of the
             # dominant launch over its time; EXACT mode issues mul and add
             # separately, so its ceiling is half the FMA-counted peak
             fl = W["flops_per_sample"] * bytes_per_launch / 16.0
             tf = fl / (avg_ms * 1e-3) / 1e12
-            out_fp64 = {"bound": "fp64", "achieved": round(tf, 2), "peak": FP64_PEAK_TFLOPS,
-                        "unit": "TFLOP/s", "frac": round(tf / FP64_PEAK_TFLOPS, 4),
-                        "flops_per_launch": fl,
-                        "exact_mode_ceiling": FP64_PEAK_TFLOPS / 2 if args.math == "exact" else None}
+            r["fp64"] = {"bound": "fp64", "achieved": round(tf, 2), "peak": FP64_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(tf / FP64_PEAK_TFLOPS, 4),
+                         "flops_per_launch": fl,
+                         "exact_mode_ceiling": FP64_PEAK_TFLOPS / 2 if math == "exact" else None}
+    return r
+
+
+def kernels_of(prof):
+    """Per-kind averages of region B (every launch evented in its packet)."""
+    return {k: {"launches": v["launches"], "avg_us": round(v["total_ms"] * 1e3 / v["launches"], 2),
+                "GBps": round(v["bytes"] / (v["total_ms"] * 1e-3) / 1e9, 1)}
+            for k, v in prof.items()}
+
+
+def secondary_configs(args, d):
+    """BASELINE configs 3, 4 (EXACT and FMA) and 5 at one GPU, each timed as
+    its own --workload run would time it (same warmup, regions A and B), in
+    compact form; no CPU legs (the per-workload runs carry those).  One
+    object per config, {"error": ...} if one fails."""
+    import copy
+    out = {}
+    for key, wl, math in (("config3_fwt2d", "fwt2d", "exact"), ("config4_wpt", "wpt", "exact"),
+                          ("config4_wpt_fma", "wpt", "fma"), ("config5_modwt", "modwt", "exact")):
+        a = copy.copy(args)
+        a.math = math
+        try:
+            W = setup(a, d, wl)
+            r = measure(a, d, W, wl, args.steps, args.warmup, math)
+            el = r["el"]
+            o = {"workload": W["config"]["workload"], "math": math,
+                 "ms_per_step": round(el / args.steps * 1e3, 4),
+                 "value": round(W["samples"] * args.steps * d.world / el, 1), "unit": "samples/s",
+                 "hbm_gbps": round(W["bytes"] * args.steps * d.world / el / 1e9, 1),
+                 "steps": args.steps, "warmup_steps_run": r["wsteps"],
+                 "roofline": r["roof"], "kernels_profiled_pass": kernels_of(r["prof"]),
+                 "roundtrip_max_abs_err": W["check"]()}
+            if r["fp64"]:
+                o["roofline_fp64"] = r["fp64"]
+            W["ctx"].close()
+            del W
+        except Exception as e:  # one config's failure must not void the metric line
+            o = {"workload": wl, "math": math, "error": "%s: %s" % (type(e).__name__, e)}
+        out[key] = o
+    return out
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    d = Dist(args.gpus, args.dry_run)
+    W = setup_dry(args, d) if args.dry_run else setup(args, d)
+    ctx = W["ctx"]
+    r = measure(args, d, W, args.workload, args.steps, args.warmup, args.math)
+    el, wsteps, prof, tb = r["el"], r["wsteps"], r["prof"], r["tb"]
+    out_roof, out_fp64, issue = r["roof"], r["fp64"], [r["issue"]]
 
     exch = None
     if W.get("exchange"):
@@ -731,10 +780,7 @@ def main():
     value = W["samples"] * args.steps * world / el
     gbps = W["bytes"] * args.steps * world / el / 1e9
     err = W["check"]()
-    # per-kind averages of region B (every launch evented in its packet)
-    kernels = {k: {"launches": v["launches"], "avg_us": round(v["total_ms"] * 1e3 / v["launches"], 2),
-                   "GBps": round(v["bytes"] / (v["total_ms"] * 1e-3) / 1e9, 1)}
-               for k, v in (prof if ctx is not None else {}).items()}
+    kernels = kernels_of(prof if ctx is not None else {})
     out = {"metric": W["metric"], "value": round(value, 1), "unit": "samples/s",
            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
            "warmup_steps_run": wsteps, "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True,
@@ -756,6 +802,10 @@ def main():
         out["batched_wpt_strong"] = secondary_wpt(args, d)
         if d.rank == 0:
             out["host_entry"] = host_entry(args, d)
+        # configs 3-5 at one GPU in the driver-timed line (their sharded
+        # multi-GPU forms are --workload runs)
+        if d.world == 1:
+            out["configs"] = secondary_configs(args, d)
     # the reference's CPU path on this node's host cores, in the same run, at
     # every world size (rank 0, after every GPU leg)
     if d.rank == 0 and W["cpu"] and not args.no_cpu_baseline:

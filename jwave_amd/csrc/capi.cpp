@@ -160,9 +160,7 @@ struct jwv_ctx {
   DevBuf hin, hout;  // device buffers of the host-pointer entry points
   PinRing pin;       // their pinned host staging (allocated on first use)
   unsigned tail_base = 0;    // fused forward tail: counter value before the next launch
-  bool tail_dirty = false;   // the call in progress enqueued a launch with arrival counters
-  unsigned* rowcnt = nullptr;  // fused row tails: one arrival counter per row, zero between launches
-  size_t rowcnt_n = 0;
+  bool tail_dirty = false;   // a tail launch was enqueued by the call in progress
   // single-launch FWT chains: [0, kWords) forward counters, [kWords, 2 kWords)
   // reverse ticket/flags; zeroed once, left zero by every completed launch
   unsigned* sync = nullptr;
@@ -417,28 +415,14 @@ unsigned* tail_counter(jwv_ctx* c) { return sync_words(c) + 2 * ChainGeo::kWords
 // counter's value is unknown.  Drain the stream and zero the counter and its
 // base together (best effort: if the device is gone the context is too).
 void tail_resync(jwv_ctx* c) {
-  if (!c->tail_dirty) return;
+  if (!c->sync || !c->tail_dirty) return;
   c->tail_dirty = false;
   int prev = -1;
   if (hipGetDevice(&prev) != hipSuccess || (prev != c->device && hipSetDevice(c->device) != hipSuccess))
     return;
   (void)hipStreamSynchronize(c->stream);
-  if (c->sync && hipMemset(tail_counter(c), 0, sizeof(unsigned)) == hipSuccess) c->tail_base = 0;
-  if (c->rowcnt) (void)hipMemset(c->rowcnt, 0, c->rowcnt_n * sizeof(unsigned));
+  if (hipMemset(tail_counter(c), 0, sizeof(unsigned)) == hipSuccess) c->tail_base = 0;
   if (prev != c->device) (void)hipSetDevice(prev);
-}
-// Arrival counters of the fused row tails (fwt1_fused.hpp): n words, zero.
-unsigned* row_counters(jwv_ctx* c, int64_t n) {
-  if (c->rowcnt_n < (size_t)n) {
-    HIPCHK(hipStreamSynchronize(c->stream));
-    if (c->rowcnt) HIPCHK(hipFree(c->rowcnt));
-    c->rowcnt = nullptr;
-    c->rowcnt_n = 0;
-    HIPCHK(hipMalloc(&c->rowcnt, (size_t)n * sizeof(unsigned)));
-    HIPCHK(hipMemsetAsync(c->rowcnt, 0, (size_t)n * sizeof(unsigned), c->stream));
-    c->rowcnt_n = (size_t)n;
-  }
-  return c->rowcnt;
 }
 
 int plan_of(jwv_ctx* c) { return c->plan >= 0 ? c->plan : ChainGeo::default_plan(); }
@@ -522,22 +506,6 @@ int fwt_res_cap(int C, int64_t outer) {
 // reverse that reads them next took 123 us/step).
 int store_pol_dir(int rev, bool final = false) { return rev && final ? 2 : 0; }
 
-// The last tiled pass over many rows takes the rows' resident remainder into
-// the same launch (fwt_fwd_tile1r) where that remainder is the wave-per-row
-// tail's case (>= 64 rows, 2..kFusedRowH samples left) and the tile is the
-// default C = 1 geometry.  Config 3 rows: tile pass + tail 204 + 35 us -> see
-// DESIGN.md §5.0.
-#ifndef JWV_FUSE_ROW_TAIL
-#define JWV_FUSE_ROW_TAIL 1
-#endif
-constexpr int kFusedRowH = 1024;  // fwt1_row.hpp kSmallH
-bool fuse_row_tail(bool f1, const Axis& a, int h, int K, int rem, int cap, const jwv::TileArgs& t) {
-  if (!JWV_FUSE_ROW_TAIL || !f1 || a.outer < 64 || t.t1 != 0 || K > 6 || rem <= K) return false;
-  const int hr = h >> K;
-  return hr >= 2 && hr <= kFusedRowH && hr <= cap && h % Geo::kFwt1T == 0 &&
-         a.outer <= (int64_t(1) << 30);
-}
-
 // FastWaveletTransform.forward's level loop (FastWaveletTransform.java:90-97)
 // as device passes.  ws: the ping-pong pair for the level approximations.
 Plan fwt_fwd_plan(jwv_ctx* c, const Bank& b, const Axis& a, int level, DevBuf* ws) {
@@ -605,25 +573,13 @@ Plan fwt_fwd_plan(jwv_ctx* c, const Bank& b, const Axis& a, int level, DevBuf* w
     const bool last = K == rem;
     double* ad = last ? a.dst : ws[pp].p;
     const AxisView av = last ? a.dv : cview(h >> K, a.inner);
-    jwv::TileArgs t{cur, cv, nullptr, {}, a.dst, a.dv, ad, av, h, K, a.outer, a.inner,
-                    dma_view(cur, cv, C, a.inner),
-                    Geo::tile_walk(),
-                    first1 && h == a.len && Geo::fwd1_first_t() != Geo::kFwt1T
-                        ? Geo::fwd1_first_t() : 0};
+    const jwv::TileArgs t{cur, cv, nullptr, {}, a.dst, a.dv, ad, av, h, K, a.outer, a.inner,
+                          dma_view(cur, cv, C, a.inner),
+                          Geo::tile_walk(),
+                          first1 && h == a.len && Geo::fwd1_first_t() != Geo::kFwt1T
+                              ? Geo::fwd1_first_t() : 0};
     const int kind = h == a.len ? K_FWT_FWD_TILE : K_FWT_FWD_TILE_DEEP;
     const double bytes = 16.0 * a.outer * h * a.inner;
-    // many rows whose remainder fits the wave-per-row tail: that tail runs
-    // in the tile launch itself (fwt_fwd_tile1r, fwt1_fused.hpp)
-    if (fuse_row_tail(f1, a, h, K, rem, cap, t)) {
-      t.rowcnt = row_counters(c, a.outer);
-      t.levr = rem - K;
-      p.push_back({false, 0, [c, &b, C, t, kind, bytes] {
-        c->tail_dirty = true;
-        ProfScope ps_(c, kind, bytes);
-        hipchk(jwv::launch_fwt_fwd_tile(b, use_fma(c), C, t, c->stream), "fwt_fwd_tile1r");
-      }});
-      return p;
-    }
     p.push_back({false, 0, [c, &b, C, t, kind, bytes] {
       ProfScope ps_(c, kind, bytes);
       hipchk(jwv::launch_fwt_fwd_tile(b, use_fma(c), C, t, c->stream), "fwt_fwd_tile");
@@ -648,23 +604,6 @@ Plan fwt_fwd_plan(jwv_ctx* c, const Bank& b, const Axis& a, int level, DevBuf* w
 
 void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
   run_plan(fwt_fwd_plan(c, b, a, level, c->ws));
-}
-
-// The resident head of many rows runs inside the first tile pass
-// (fwt_rev_tile1h) where it is the wave-per-row tail's case (>= 64 rows, a
-// head of 2..kFusedRowH outputs) and that pass is a C = 1 tile pass of at
-// most 4 levels; every tile recomputes its row's head (no inter-workgroup
-// wait).
-#ifndef JWV_FUSE_ROW_HEAD
-#define JWV_FUSE_ROW_HEAD 1
-#endif
-bool fuse_row_head(bool f1, const Axis& a, int h, int cap, int KM, int C) {
-  if (!JWV_FUSE_ROW_HEAD || !f1 || C != 1 || a.outer < 64) return false;
-  const int hres = std::min(a.len, cap);
-  if (hres < 2 || hres > kFusedRowH || hres >= a.len || h < 1) return false;
-  const int h1 = hres * 2, K = std::min(exponent(a.len / h1) + 1, KM);
-  return K <= 4 && ((int64_t)h1 << (K - 1)) % Geo::kRev1T == 0 &&
-         dma_view(a.src, a.sv, 1, 1) && a.outer <= (int64_t(1) << 30);
 }
 
 // FastWaveletTransform.reverse's level loop (FastWaveletTransform.java:137-149).
@@ -708,7 +647,7 @@ Plan fwt_rev_plan(jwv_ctx* c, const Bank& b, const Axis& a, int level, DevBuf* w
   }
   const double* acur;
   AxisView acv;
-  int h1, pp = 0, head_h0 = 0, head_nlev = 0;
+  int h1, pp = 0;
   // JWV_PLAN_REV_HEAD: the resident pass and the first tiled pass (kFwt1KMax
   // levels, fwt1 geometry) fused into one launch (fwt_rev_head1); the
   // remaining tiled passes follow as below.
@@ -727,14 +666,6 @@ Plan fwt_rev_plan(jwv_ctx* c, const Bank& b, const Axis& a, int level, DevBuf* w
     acur = out;
     acv = cview(hM, 1);
     h1 = hM * 2;
-  } else if (h <= cap && fuse_row_head(f1, a, h, cap, KM, C)) {
-    // the rows' resident head runs inside the first tile pass (fwt_rev_tile1h)
-    const int hres = std::min(a.len, cap);
-    head_h0 = h;
-    head_nlev = exponent(hres / h) + 1;
-    acur = nullptr;
-    acv = cview(hres, a.inner);
-    h1 = hres * 2;
   } else if (h <= cap) {
     const int hres = std::min(a.len, cap);
     const int nres = exponent(hres / h) + 1;
@@ -764,13 +695,10 @@ Plan fwt_rev_plan(jwv_ctx* c, const Bank& b, const Axis& a, int level, DevBuf* w
     const bool last = hK == a.len;
     double* out = last ? a.dst : ws[pp].p;
     const AxisView ov = last ? a.dv : cview(hK, a.inner);
-    jwv::TileArgs t{acur, acv, a.src, a.sv, out, ov, nullptr, {}, h1, K, a.outer, a.inner,
-                    (!acur || dma_view(acur, acv, C, a.inner)) && dma_view(a.src, a.sv, C, a.inner),
-                    (last ? store_pol_dir(1, a.outer == 1 && a.inner == 1) : 0) |
-                        Geo::tile_walk()};
-    t.head_h0 = head_h0;
-    t.head_nlev = head_nlev;
-    head_nlev = 0;
+    const jwv::TileArgs t{acur, acv, a.src, a.sv, out, ov, nullptr, {}, h1, K, a.outer, a.inner,
+                          dma_view(acur, acv, C, a.inner) && dma_view(a.src, a.sv, C, a.inner),
+                          (last ? store_pol_dir(1, a.outer == 1 && a.inner == 1) : 0) |
+                              Geo::tile_walk()};
     const int kind = last ? K_FWT_REV_TILE : K_FWT_REV_TILE_DEEP;
     const double bytes = 16.0 * a.outer * hK * a.inner;
     p.push_back({false, 0, [c, &b, C, t, kind, bytes] {
@@ -1402,7 +1330,6 @@ hipError_t launch_fwt_fwd_tile(const Bank& b, bool fma, int C, const TileArgs& a
   hipError_t e = hipSuccess;
   if (C == 1 && (fma ? fused::fwt_fwd_tile1(b, a, s, e) : exact::fwt_fwd_tile1(b, a, s, e)))
     return e;
-  if (a.rowcnt) return hipErrorInvalidValue;  // the fused row tail has no generic kernel
   if (C == 8 && (fma ? fused::fwt_tile8(b, a, s, true, e) : exact::fwt_tile8(b, a, s, true, e)))
     return e;
   // the generic kernels are compiled for at most fwt_k(C) fused levels
@@ -1413,7 +1340,6 @@ hipError_t launch_fwt_rev_tile(const Bank& b, bool fma, int C, const TileArgs& a
   hipError_t e = hipSuccess;
   if (C == 1 && (fma ? fused::fwt_rev_tile1(b, a, s, e) : exact::fwt_rev_tile1(b, a, s, e)))
     return e;
-  if (a.head_nlev) return hipErrorInvalidValue;  // the fused row head has no generic kernel
   if (C == 8 && (fma ? fused::fwt_tile8(b, a, s, false, e) : exact::fwt_tile8(b, a, s, false, e)))
     return e;
   if (a.K > Geo::fwt_k(C)) return hipErrorInvalidValue;
@@ -1517,7 +1443,6 @@ int jwv_ctx_destroy(jwv_ctx* c) {
   for (DevBuf* b : {&c->ws[0], &c->ws[1], &c->big, &c->big2, &c->red, &c->hin, &c->hout})
     if (b->p) hipFree(b->p);
   if (c->sync) hipFree(c->sync);
-  if (c->rowcnt) hipFree(c->rowcnt);
   for (auto& r : c->recs) { hipEventDestroy(r.e0); hipEventDestroy(r.e1); }
   for (auto e : c->ev_pool) hipEventDestroy(e);
   for (int i = 0; i < kPinSlots; ++i) {

@@ -71,15 +71,6 @@ struct TileArgs {  // tiled FWT/WPT kernels
   int dma;
   int sp = 0;  // cache policy of the full-length output stores (st2_pol), C = 1 kernels
   int t1 = 0;  // C = 1 forward tile: 0 = Geo::kFwt1T, or 1024 (first pass of a long signal)
-  // C = 1 forward tile of many rows with the rows' resident tail fused
-  // (fwt_fwd_tile1r, fwt1_fused.hpp): one arrival counter per row (zero
-  // between launches), levr resident levels after the K tiled ones
-  unsigned* rowcnt = nullptr;
-  int levr = 0;
-  // C = 1 reverse tile of many rows with the rows' resident head fused
-  // (fwt_rev_tile1h): head levels of output size head_h0 .. hK >> K from the
-  // coefficient prefix (src unused)
-  int head_h0 = 0, head_nlev = 0;
 };
 // AncientEgyptianDecomposition varlen launch (aed_kernels.hpp): contiguous
 // 1-D segments of src / dst, one block each.

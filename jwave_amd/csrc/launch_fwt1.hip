@@ -4,7 +4,6 @@
 // column-slab tiles live in launch_wpt1.hip / launch_fwt8.hip).  Used for contiguous, 16-B aligned signals with a
 // compiled-in tap count; every other case keeps the generic tile kernels.
 #include "fwt1_kernels.hpp"
-#include "fwt1_fused.hpp"
 #include <cstdlib>
 #include "fwt1_res.hpp"
 #include "fwt1_row.hpp"
@@ -44,36 +43,9 @@ hipError_t fwd1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
                      a.av.s_outer, a.h, tp, a.sp);
   return hipGetLastError();
 }
-// tile pass + the rows' resident tail in one launch (fwt1_fused.hpp)
-template <int L, int NT, int T, int K>
-hipError_t fwd1r_k(const Bank& b, const TileArgs& a, hipStream_t s) {
-  auto k = fwt_fwd_tile1r<L, NT, T, K, kFMA>;
-  const size_t lds = (size_t)Fwd1Geo<L, T, K>::lds_doubles() * sizeof(double);
-  if (hipError_t e = prep1(k, lds)) return e;
-  FwdTaps<L> tp;
-  for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
-  const dim3 grid((unsigned)(a.nouter * (a.h / T)));
-  JWV_LAUNCH(k, grid, dim3(NT), lds, s, a.src, a.sv.s_outer, a.dst, a.dv.s_outer, a.adst,
-                     a.av.s_outer, a.h, tp, a.sp, a.rowcnt, a.levr);
-  return hipGetLastError();
-}
-template <int L>
-hipError_t fwd1r_l(const Bank& b, const TileArgs& a, hipStream_t s) {
-  constexpr int NT = 256, T = kFwdT;
-  switch (a.K) {
-    case 1: return fwd1r_k<L, NT, T, 1>(b, a, s);
-    case 2: return fwd1r_k<L, NT, T, 2>(b, a, s);
-    case 3: return fwd1r_k<L, NT, T, 3>(b, a, s);
-    case 4: return fwd1r_k<L, NT, T, 4>(b, a, s);
-    case 5: return fwd1r_k<L, NT, T, 5>(b, a, s);
-    case 6: return fwd1r_k<L, NT, T, 6>(b, a, s);
-    default: return hipErrorInvalidValue;
-  }
-}
 template <int L>
 hipError_t fwd1_l(const Bank& b, const TileArgs& a, hipStream_t s) {
   constexpr int NT = 256, T = kFwdT;
-  if (a.rowcnt) return fwd1r_l<L>(b, a, s);
   if (a.t1 == 1024) {  // first pass of a long signal (Geo::fwd1_first_t)
     switch (a.K) {
       case 4: return fwd1_k<L, NT, 1024, 4>(b, a, s);
@@ -111,34 +83,9 @@ hipError_t rev1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
                      a.dv.s_outer, hK, tp, a.sp);
   return hipGetLastError();
 }
-template <int L, int NT, int T, int K>
-hipError_t rev1h_k(const Bank& b, const TileArgs& a, hipStream_t s) {
-  auto k = fwt_rev_tile1h<L, NT, T, K, kFMA>;
-  const int hK = a.h << (a.K - 1);
-  const size_t lds = (size_t)rev1h_lds_doubles<L, T, K>(hK >> K) * sizeof(double);
-  if (hipError_t e = prep1(k, lds)) return e;
-  RevTaps<L> tp;
-  for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
-  const dim3 grid((unsigned)(a.nouter * (hK / T)));
-  JWV_LAUNCH(k, grid, dim3(NT), lds, s, a.coef, a.cv.s_outer, a.dst, a.dv.s_outer, hK,
-                     a.head_h0, a.head_nlev, tp, a.sp);
-  return hipGetLastError();
-}
-template <int L>
-hipError_t rev1h_l(const Bank& b, const TileArgs& a, hipStream_t s) {
-  constexpr int NT = 256, T = kRevT;
-  switch (a.K) {
-    case 1: return rev1h_k<L, NT, T, 1>(b, a, s);
-    case 2: return rev1h_k<L, NT, T, 2>(b, a, s);
-    case 3: return rev1h_k<L, NT, T, 3>(b, a, s);
-    case 4: return rev1h_k<L, NT, T, 4>(b, a, s);
-    default: return hipErrorInvalidValue;
-  }
-}
 template <int L>
 hipError_t rev1_l(const Bank& b, const TileArgs& a, hipStream_t s) {
   constexpr int NT = 256, T = kRevT;
-  if (a.head_nlev) return rev1h_l<L>(b, a, s);
   switch (a.K) {
     case 1: return rev1_k<L, NT, T, 1>(b, a, s);
     case 2: return rev1_k<L, NT, T, 2>(b, a, s);
@@ -201,9 +148,6 @@ bool fwt_fwd_tile1(const Bank& b, const TileArgs& a, hipStream_t s, hipError_t& 
     return false;
   if (a.t1 != 0 && (a.t1 != 1024 || a.K < 4 || a.K > 6)) return false;
   if (a.h % (a.t1 ? a.t1 : kFwdT)) return false;
-  // fused row tail: the wave-per-row tail's domain (<= kSmallH samples left)
-  if (a.rowcnt && (a.t1 || a.K > 6 || a.levr < 1 || (a.h >> a.K) > kSmallH || (a.h >> a.K) < 2))
-    return false;
   switch (b.L) {
     case 2: err = fwd1_l<2>(b, a, s); return true;
     case 4: err = fwd1_l<4>(b, a, s); return true;
@@ -292,12 +236,6 @@ bool fwt_rev_tile1(const Bank& b, const TileArgs& a, hipStream_t s, hipError_t& 
   if (!plain(a.sv) || !plain(a.cv) || !plain(a.dv) || a.K < 1 || a.K > Geo::kFwt1KMax) return false;
   if (((uintptr_t)a.dst & 15) || !even_rows(a.dv, a.nouter)) return false;
   if ((a.h << (a.K - 1)) % kRevT) return false;
-  if (a.head_nlev) {  // fused head: the wave-per-row domain, coefficient rows 16-B aligned
-    const int64_t hR = (int64_t)a.h >> 1;  // = hK >> K
-    if (a.K > 4 || a.head_h0 < 1 || ((int64_t)a.head_h0 << (a.head_nlev - 1)) != hR ||
-        hR > kSmallH || hR < 2 || ((uintptr_t)a.coef & 15) || !even_rows(a.cv, a.nouter))
-      return false;
-  }
   switch (b.L) {
     case 2: err = rev1_l<2>(b, a, s); return true;
     case 4: err = rev1_l<4>(b, a, s); return true;
