@@ -477,10 +477,16 @@ def test_modwt_config5_full_size(ctx, ctx_fma):
     assert d <= RT_GATE, "config 5 FMA round trip vs oracle round trip: %g" % d
 
 
-@pytest.mark.parametrize("n", [1_000_003, 2_097_152, 3_333_331])
+@pytest.mark.parametrize("n", [5_634, 5_636, 5_638, 6_146, 1_000_002, 1_000_003, 2_097_152,
+                               3_333_331])
 def test_modwt_chunked_sizes(ctx, n):
-    """J = 8 signals of many 512-sample tiles: inverse chunks of several tiles,
-    chunk ends inside and at the end of the signal (wrap), ragged last tile."""
+    """J = 8, Daubechies4.  Even N take the streamed forward (modwt_stream.hpp,
+    1024-sample tiles walked left to right with carried halos, one chunk per
+    resident block); its minimum is N = 2 (XP + Wn(1)) = 2 (1786 + 1032) =
+    5636, where the prologue and the first tile's wrap are tightest (5634:
+    the tile kernel; 5638, 6146: one and a few tiles past the minimum, ragged
+    last tile; 1_000_002: many chunks, ragged last tile).  Odd N take the tile
+    kernel.  The inverse is the tile kernel at every N."""
     w = jw.by_class("Daubechies4")
     x = rnd(n, 5)
     cr = oracle.modwt_forward(w, x, 8)
