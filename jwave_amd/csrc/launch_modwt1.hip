@@ -52,13 +52,13 @@ hipError_t fwd_kp(const Bank& b, const ModwtArgs& a, hipStream_t s) {
   JWV_LAUNCH(k, grid, dim3(NT), lds, s, a.src, a.wout, a.ldw, a.vout, a.N, taps<L>(b));
   return hipGetLastError();
 }
-template <int L, int J1, int M, int NT = kNT, int TI = kTI>
+template <int L, int J1, int M>
 hipError_t inv_kp(const Bank& b, const ModwtArgs& a, hipStream_t s) {
-  auto k = modwt_inv_tile1<L, NT, TI, 1, J1, kFMA, true, M>;
-  const size_t lds = (size_t)ModInv1Geo<L, TI, 1, J1>::lds_doubles(M) * sizeof(double);
+  auto k = modwt_inv_tile1<L, kNT, kTI, 1, J1, kFMA, true, M>;
+  const size_t lds = (size_t)ModInv1Geo<L, kTI, 1, J1>::lds_doubles(M) * sizeof(double);
   if (hipError_t e = prep(k, lds)) return e;
-  const dim3 grid((unsigned)((a.N + TI - 1) / TI));
-  JWV_LAUNCH(k, grid, dim3(NT), lds, s, a.src, a.coef, a.ldw, a.vout, a.N, taps<L>(b));
+  const dim3 grid((unsigned)((a.N + kTI - 1) / kTI));
+  JWV_LAUNCH(k, grid, dim3(kNT), lds, s, a.src, a.coef, a.ldw, a.vout, a.N, taps<L>(b));
   return hipGetLastError();
 }
 
@@ -117,22 +117,9 @@ hipError_t fwd_k(const Bank& b, const ModwtArgs& a, hipStream_t s) {
   }
   return fwd_kp<L, J1, kNT, kTF>(b, a, s);
 }
-#ifndef JWV_MODINV_WG
-#define JWV_MODINV_WG 1
-#endif
-#ifndef JWV_MODINV_T
-#define JWV_MODINV_T 2048
-#endif
-#ifndef JWV_MODINV_NT
-#define JWV_MODINV_NT 512
-#endif
 template <int L, int J1>
 hipError_t inv_k(const Bank& b, const ModwtArgs& a, hipStream_t s) {
-  if constexpr (J1 == 8) {
-    if constexpr (JWV_MODINV_WG)
-      return inv_kp<L, J1, 1303, JWV_MODINV_NT, JWV_MODINV_T>(b, a, s);
-    return inv_kp<L, J1, 303>(b, a, s);
-  }
+  if constexpr (J1 == 8) return inv_kp<L, J1, 303>(b, a, s);
   return inv_kp<L, J1, 1>(b, a, s);
 }
 template <int L, bool FWD>

@@ -137,7 +137,6 @@ struct ModFwd1Level {
   // M = m + 100*jr: run form with m pairs per lane on levels j >= jr
   static constexpr int kM = M % 100, kJR = (M / 100) % 10;
   static constexpr bool kRun = kM > 1 && j >= kJR;
-  static constexpr bool kWG = (M / 1000) % 10 == 1;  // W taps from global memory
   __device__ __forceinline__ static void run_p2(const ModwtTaps<L>& tp, double* lds,
                                                 double* __restrict__ wout, int64_t ldw,
                                                 int64_t t0, int64_t N) {
@@ -258,31 +257,6 @@ __global__ __launch_bounds__(NT) void modwt_fwd_tile1(const double* __restrict__
 }
 
 // ---------------------------------------------------------------- inverse
-// W_j taps of an inverse tile straight from global memory (M / 1000 == 1:
-// no W window in LDS, so a block holds only its V window).  pair(e) = the
-// two doubles at window offsets (e, e + 1), e even: one 16-B buffer load for
-// tiles inside the signal (the resource's extent ends at N, so a run's reads
-// past the last output read zeros, never another row), the periodic index per
-// double for the tiles that wrap.  Neighbouring lanes read neighbouring
-// slots and a tile's taps overlap 8-fold, so L1 / L2 serve most of it.
-struct ModWSrc {
-  const double* row;
-  __amdgpu_buffer_rsrc_t rs;
-  int64_t t0, N;
-  bool inside;
-  __device__ __forceinline__ ModWSrc(const double* row_, int64_t t0_, int64_t N_, bool inside_)
-      : row(row_), t0(t0_), N(N_), inside(inside_) {
-    const int64_t ext = (N_ - t0_) * 8;
-    rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(row_ + t0_), 0,
-                                           (int)(ext > 0x7ffffff0 ? 0x7ffffff0 : ext), 0x00020000);
-  }
-  __device__ __forceinline__ double2 pair(int e) const {
-    if (inside)
-      return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, e * 8, 0, 0));
-    return make_double2(row[wrap_mod(t0 + e, N)], row[wrap_mod(t0 + e + 1, N)]);
-  }
-};
-
 // Levels J1 down to J0.  Window of level j: T outputs + right halo Rin(j) =
 // (L-1)(2^j - 2^(J0-1)); its outputs carry Rout(j) = Rin(j) - (L-1)2^(j-1).
 // LDS: vb (V window, in place) and wb (this level's W window).  The next
@@ -312,7 +286,6 @@ struct ModInv1Geo {
     return b;
   }
   static constexpr int lds_doubles(int M) {
-    if ((M / 1000) % 10 == 1) return M % 100 > 1 ? run_buf(M) : buf();  // W from global
     return M % 100 > 1 ? 2 * run_buf(M) : lds_doubles();
   }
 };
@@ -324,7 +297,6 @@ struct ModInv1Level {
   // M = m + 100*jr: run form with m pairs per lane on levels j >= jr
   static constexpr int kM = M % 100, kJR = (M / 100) % 10;
   static constexpr bool kRun = kM > 1 && j >= kJR;
-  static constexpr bool kWG = (M / 1000) % 10 == 1;  // W taps from global memory
   static constexpr int MAXP = (G::Wmax + NT - 1) / NT;
   // fetch the W_j window [t0, t0 + T + Rin(j)) into registers
   __device__ __forceinline__ static void fetch(double (&pw)[MAXP], const double* __restrict__ coef,
@@ -362,38 +334,26 @@ struct ModInv1Level {
                                              int64_t ldw, double* __restrict__ dst, int64_t t0,
                                              int64_t N, bool inside) {
     static_assert(P2, "inverse: the P2 or run form");
-    if constexpr (kWG) {
-      JWV_MOD_BAR();  // the V window (loaded, or the previous level's outputs) is complete
-      const ModWSrc ws(coef + (int64_t)(j - 1) * ldw, t0, N, inside);
-      auto wr = [&](int e) { return ws.pair(e); };
-      if constexpr (kRun)
-        compute_mr(tp, vb, wr, pw, coef, ldw, dst, t0, N, inside);
-      else
-        compute_p2(tp, vb, wr, pw, coef, ldw, dst, t0, N, inside);
-    } else {
-      constexpr int Wn = T + G::Rin(j);
-      const int tid = opaque_tid();
+    constexpr int Wn = T + G::Rin(j);
+    const int tid = opaque_tid();
 #pragma unroll
-      for (int r = 0; r < MAXP; ++r) {
-        const int q = tid + r * NT;
-        if (r * NT < Wn && ((r + 1) * NT <= Wn || q < Wn)) wb[q] = pw[r];
-      }
-      JWV_MOD_BAR();
-      if constexpr (j > J0)
-        ModInv1Level<L, NT, T, J0, J1, FMA, j - 1, P2, M>::fetch(pw, coef, ldw, t0, N, inside);
-      auto wr = [&](int e) { return *reinterpret_cast<const double2*>(wb + e); };
-      if constexpr (kRun)
-        compute_mr(tp, vb, wr, pw, coef, ldw, dst, t0, N, inside);
-      else
-        compute_p2(tp, vb, wr, pw, coef, ldw, dst, t0, N, inside);
+    for (int r = 0; r < MAXP; ++r) {
+      const int q = tid + r * NT;
+      if (r * NT < Wn && ((r + 1) * NT <= Wn || q < Wn)) wb[q] = pw[r];
     }
+    JWV_MOD_BAR();
+    if constexpr (j > J0)
+      ModInv1Level<L, NT, T, J0, J1, FMA, j - 1, P2, M>::fetch(pw, coef, ldw, t0, N, inside);
+    if constexpr (kRun)
+      compute_mr(tp, vb, wb, pw, coef, ldw, dst, t0, N, inside);
+    else
+      compute_p2(tp, vb, wb, pw, coef, ldw, dst, t0, N, inside);
   }
   // P2: a lane computes the adjacent outputs (p, p+1), p even: every tap pair
   // (p + l*st, p + 1 + l*st) of V and of W is one 16-B LDS read (st = 1: the
   // 10-value runs p .. p+9), 16-B lane stride.  An odd output count leaves
   // one extra output at index nout, past what the next level reads.
-  template <typename WR>
-  __device__ __forceinline__ static void compute_p2(const ModwtTaps<L>& tp, double* vb, WR wr,
+  __device__ __forceinline__ static void compute_p2(const ModwtTaps<L>& tp, double* vb, double* wb,
                                                     double (&pw)[MAXP],
                                                     const double* __restrict__ coef, int64_t ldw,
                                                     double* __restrict__ dst, int64_t t0,
@@ -410,13 +370,14 @@ struct ModInv1Level {
       const bool full = (r + 1) * NT <= NP;
       const int kc = full ? k : (k < NP ? k : NP - 1);
       const double* a = vb + 2 * kc;
+      const double* w = wb + 2 * kc;
       double av0[L], av1[L], aw0[L], aw1[L];
       if constexpr (st == 1) {
         double va[L + 2], vw[L + 2];
 #pragma unroll
         for (int i = 0; i < L + 2; i += 2) {
           const double2 u = *reinterpret_cast<const double2*>(a + i);
-          const double2 z = wr(2 * kc + i);
+          const double2 z = *reinterpret_cast<const double2*>(w + i);
           va[i] = u.x;
           va[i + 1] = u.y;
           vw[i] = z.x;
@@ -433,7 +394,7 @@ struct ModInv1Level {
 #pragma unroll
         for (int l = 0; l < L; ++l) {
           const double2 u = *reinterpret_cast<const double2*>(a + l * st);
-          const double2 z = wr(2 * kc + l * st);
+          const double2 z = *reinterpret_cast<const double2*>(w + l * st);
           av0[l] = u.x;
           av1[l] = u.y;
           aw0[l] = z.x;
@@ -478,20 +439,15 @@ struct ModInv1Level {
         const int k = tid + r * NT;
         if ((r + 1) * NT <= NP || k < NP) *reinterpret_cast<double2*>(vb + 2 * k) = vv[r];
       }
-      ModInv1Level<L, NT, T, J0, J1, FMA, j - 1, P2, M>::run(tp, vb, next_wb(vb), pw, coef, ldw,
-                                                          dst, t0, N, inside);
+      ModInv1Level<L, NT, T, J0, J1, FMA, j - 1, P2, M>::run(tp, vb, wb, pw, coef, ldw, dst, t0, N,
+                                                          inside);
     }
-  }
-  // the W window buffer after the V window (unused when the taps come from
-  // global memory)
-  __device__ __forceinline__ static double* next_wb(double* vb) {
-    return vb + (M % 100 > 1 ? G::run_buf(M) : G::buf());
   }
   // Run form (ModRun): output pair slot s = s0 + m*h, m < M, reads tap slots
   // s0 + k*h, k < M + L - 1 (st = 1: doubles 2*s0 .. 2*s0 + 2M + L - 1).
   // V taps first, then W taps (registers: one operand's run at a time).
-  template <bool ISW, typename RD>
-  __device__ __forceinline__ static void run_sums(const ModwtTaps<L>& tp, RD rd,
+  template <bool ISW>
+  __device__ __forceinline__ static void run_sums(const ModwtTaps<L>& tp, const double* base,
                                                   double (&acc)[kM][2]) {
     constexpr int st = 1 << (j - 1);
     constexpr int H = ModRun<L, kM>::template h<st>();
@@ -499,7 +455,7 @@ struct ModInv1Level {
     double v[2 * NRD];
 #pragma unroll
     for (int k = 0; k < NRD; ++k) {
-      const double2 u = rd(2 * k * H);
+      const double2 u = *reinterpret_cast<const double2*>(base + 2 * k * H);
       v[2 * k] = u.x;
       v[2 * k + 1] = u.y;
     }
@@ -519,8 +475,7 @@ struct ModInv1Level {
       }
     }
   }
-  template <typename WR>
-  __device__ __forceinline__ static void compute_mr(const ModwtTaps<L>& tp, double* vb, WR wr,
+  __device__ __forceinline__ static void compute_mr(const ModwtTaps<L>& tp, double* vb, double* wb,
                                                     double (&pw)[MAXP],
                                                     const double* __restrict__ coef, int64_t ldw,
                                                     double* __restrict__ dst, int64_t t0,
@@ -544,9 +499,8 @@ struct ModInv1Level {
       const int tc = full ? t : (t < NTASK ? t : NTASK - 1);
       const int s0 = ModRun<L, kM>::template slot0<st>(tc);
       double sa[kM][2], sd[kM][2];
-      const double* va = vb + 2 * s0;
-      run_sums<false>(tp, [&](int e) { return *reinterpret_cast<const double2*>(va + e); }, sa);
-      run_sums<true>(tp, [&](int e) { return wr(2 * s0 + e); }, sd);
+      run_sums<false>(tp, vb + 2 * s0, sa);
+      run_sums<true>(tp, wb + 2 * s0, sd);
 #pragma unroll
       for (int m = 0; m < kM; ++m) {
         pin2(sa[m][0], sd[m][0]);
@@ -583,8 +537,8 @@ struct ModInv1Level {
       }
     }
     if constexpr (j > J0)
-      ModInv1Level<L, NT, T, J0, J1, FMA, j - 1, P2, M>::run(tp, vb, next_wb(vb), pw, coef, ldw,
-                                                          dst, t0, N, inside);
+      ModInv1Level<L, NT, T, J0, J1, FMA, j - 1, P2, M>::run(tp, vb, wb, pw, coef, ldw, dst, t0, N,
+                                                          inside);
   }
 };
 
@@ -607,7 +561,7 @@ __global__ __launch_bounds__(NT) void modwt_inv_tile1(const double* __restrict__
   else
     load_window<1, NT, Top::MAXP>(vb, vsrc, G::Wmax, false, 0, 1,
                                   [&](int e) { return wrap_mod(t0 + e, N); });
-  if constexpr (!Top::kWG) Top::fetch(pw, coef, ldw, t0, N, inside);
+  Top::fetch(pw, coef, ldw, t0, N, inside);
   Top::run(tp, vb, wb, pw, coef, ldw, dst, t0, N, inside);
 }
 
