@@ -255,6 +255,9 @@ __global__ __launch_bounds__(NT, MINW) void fwt_rev_chain1(const double* __restr
 // and the whole-transform chains above when the data is MALL-warm.
 // ====================================================================
 
+#ifndef JWV_TAIL_XCD
+#define JWV_TAIL_XCD 1
+#endif
 // Forward tail: B units (tiles of TB level-input samples, KB levels; input =
 // the big pass's approximation, written by the previous launch) and, in the
 // block that completes the counter, the resident C levels.  Grid: hB / TB.
@@ -267,7 +270,14 @@ __global__ __launch_bounds__(NT) void fwt_fwd_tail1(const double* __restrict__ s
                                                     int levC, FwdTaps<L> tp) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   using GB = Fwd1Geo<L, TB, KB>;
-  const int tid = threadIdx.x, u = blockIdx.x;
+  // XCD x (blocks b = x mod 8) takes the contiguous units [x nU/8, (x+1) nU/8):
+  // a unit's halo (up to (L-2)(2^KB - 1) samples past its TB own ones, 1.5 x
+  // TB at L = 8, KB = 9) is its neighbours' input, fetched into the same L2
+  // (round-robin dealing put every neighbour on another XCD: 2.6 x the input
+  // from the fabric, r05g)
+  const int tid = threadIdx.x, nU = gridDim.x;
+  const int u = JWV_TAIL_XCD && (nU & 7) == 0 ? (blockIdx.x & 7) * (nU >> 3) + (blockIdx.x >> 3)
+                                             : (int)blockIdx.x;
   int* ctl = reinterpret_cast<int*>(lds + tail_ctl_off<L, TB, KB>(hB >> KB));
   {
     const int msk = hB - 1, base = u * TB;
