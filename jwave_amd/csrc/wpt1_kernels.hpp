@@ -32,53 +32,6 @@ struct Wpt1FwdGeo {
   static_assert((L & 1) == 0 && ((T >> K) & 1) == 0, "even windows");
 };
 
-// A couple's four sums (pairs at x and x + 2, analysis lo / hi) with the
-// products of G taps issued ahead of their adds: per group 4G independent
-// multiplies, then the 4G adds in the per-output order (j ascending), so no
-// add waits on the multiply issued just before it and the four chains
-// alternate.  Same operations and order per output as fwd_pair (bit-exact).
-#ifndef JWV_WPT_FPIPE
-#define JWV_WPT_FPIPE 2
-#endif
-template <int L, bool FMA, int G>
-__device__ __forceinline__ void fwd_couple_pipe(const FwdTaps<L>& tp, const double* x,
-                                                double& a0, double& d0, double& a1, double& d1) {
-  static_assert(L % G == 0, "tap groups");
-  double sa0 = 0.0, sd0 = 0.0, sa1 = 0.0, sd1 = 0.0;
-#pragma unroll
-  for (int j0 = 0; j0 < L; j0 += G) {
-    double pa0[G], pd0[G], pa1[G], pd1[G];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      pa0[g] = x[j0 + g] * tp.lo[j0 + g];
-      pd0[g] = x[j0 + g] * tp.hi[j0 + g];
-      pa1[g] = x[j0 + g + 2] * tp.lo[j0 + g];
-      pd1[g] = x[j0 + g + 2] * tp.hi[j0 + g];
-    }
-#pragma unroll
-    for (int g = 0; g < G; ++g) asm volatile("" : "+v"(pa0[g]), "+v"(pd0[g]), "+v"(pa1[g]), "+v"(pd1[g]));
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      if constexpr (FMA) {  // FMA mode keeps its fused form (its own order: fwd_pair's)
-        sa0 = __builtin_fma(x[j0 + g], tp.lo[j0 + g], sa0);
-        sd0 = __builtin_fma(x[j0 + g], tp.hi[j0 + g], sd0);
-        sa1 = __builtin_fma(x[j0 + g + 2], tp.lo[j0 + g], sa1);
-        sd1 = __builtin_fma(x[j0 + g + 2], tp.hi[j0 + g], sd1);
-      } else {
-        sa0 = sa0 + pa0[g];
-        sd0 = sd0 + pd0[g];
-        sa1 = sa1 + pa1[g];
-        sd1 = sd1 + pd1[g];
-      }
-    }
-    asm volatile("" : "+v"(sa0), "+v"(sd0), "+v"(sa1), "+v"(sd1));
-  }
-  a0 = sa0;
-  d0 = sd0;
-  a1 = sa1;
-  d1 = sd1;
-}
-
 template <int L, int NT, int T, int K, bool FMA, int l>
 struct Wpt1FwdLevel {
   // lds: 2^(l-1) input sub-windows of m(l-1) samples (stride m(l-1)).
@@ -196,65 +149,6 @@ __device__ __forceinline__ void rev_couple_ilv(const RevTaps<L>& tp, const doubl
     if (q < QO) {
       so0 += mac<FMA>(a0 * FB<L>::lor(tp, 2 * q + 1), d0, FB<L>::hir(tp, 2 * q + 1));
       so1 += mac<FMA>(a1 * FB<L>::lor(tp, 2 * q + 1), d1, FB<L>::hir(tp, 2 * q + 1));
-    }
-    asm volatile("" : "+v"(se0), "+v"(so0), "+v"(se1), "+v"(so1));
-  }
-  e0 = se0;
-  o0 = so0;
-  e1 = se1;
-  o1 = so1;
-}
-
-// rev_couple_ilv with the products of G terms issued ahead of their adds:
-// per group 8G independent multiplies (a*lor, d*hir of both pairs, even and
-// odd outputs), then the 4G term sums a*lor + d*hir, then the 4G accumulator
-// adds; each output keeps its order (q descending) and its operations
-// (EXACT only; bit-exact with rev_couple_ilv).
-#ifndef JWV_WPT_RPIPE
-#define JWV_WPT_RPIPE 2
-#endif
-template <int L, int G>
-__device__ __forceinline__ void rev_couple_pipe(const RevTaps<L>& tp, const double* A,
-                                                const double* D, double& e0, double& o0,
-                                                double& e1, double& o1) {
-  constexpr int Q = L / 2;
-  static_assert(L % 2 == 0 && Q % G == 0, "even bank, whole term groups");
-  double se0 = 0.0, so0 = 0.0, se1 = 0.0, so1 = 0.0;
-#pragma unroll
-  for (int q0 = Q - 1; q0 >= 0; q0 -= G) {
-    double ta0[G], ua0[G], ta1[G], ua1[G], tb0[G], ub0[G], tb1[G], ub1[G];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const int q = q0 - g;
-      const double a0 = A[-q], d0 = D[-q], a1 = A[1 - q], d1 = D[1 - q];
-      ta0[g] = a0 * tp.lo_r[2 * q];
-      ua0[g] = d0 * tp.hi_r[2 * q];
-      ta1[g] = a1 * tp.lo_r[2 * q];
-      ua1[g] = d1 * tp.hi_r[2 * q];
-      tb0[g] = a0 * tp.lo_r[2 * q + 1];
-      ub0[g] = d0 * tp.hi_r[2 * q + 1];
-      tb1[g] = a1 * tp.lo_r[2 * q + 1];
-      ub1[g] = d1 * tp.hi_r[2 * q + 1];
-    }
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      asm volatile("" : "+v"(ta0[g]), "+v"(ua0[g]), "+v"(ta1[g]), "+v"(ua1[g]));
-      asm volatile("" : "+v"(tb0[g]), "+v"(ub0[g]), "+v"(tb1[g]), "+v"(ub1[g]));
-    }
-    double ve0[G], ve1[G], vo0[G], vo1[G];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      ve0[g] = ta0[g] + ua0[g];
-      ve1[g] = ta1[g] + ua1[g];
-      vo0[g] = tb0[g] + ub0[g];
-      vo1[g] = tb1[g] + ub1[g];
-    }
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      se0 += ve0[g];
-      se1 += ve1[g];
-      so0 += vo0[g];
-      so1 += vo1[g];
     }
     asm volatile("" : "+v"(se0), "+v"(so0), "+v"(se1), "+v"(so1));
   }
