@@ -109,6 +109,8 @@ for _s in ("", "_dev"):
 for _n in ("modwt_fwd", "modwt_inv"):
     for _s in ("", "_dev"):
         _SIGS["jwv_%s_f64%s" % (_n, _s)] = [_dp, _dp, _i64, _int, _TP, _CTX]
+for _n in ("fwd", "rev"):
+    _SIGS["jwv_fwt_rows_seg_%s_f64_dev" % _n] = [_dp, _dp, _i64, _i64, _int, _i64, _TP, _CTX]
 
 _MCTX = ctypes.c_void_p
 _SIGS.update({

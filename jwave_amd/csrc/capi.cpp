@@ -339,6 +339,11 @@ struct Axis {
   int64_t outer;
   int len;
   int inner;
+  // segmented coefficient rows (C = 1 row passes only; forward: dst, reverse:
+  // src): sample i of row o at base + o * s_outer + (i >> lsw) * ss + (i mod
+  // 2^lsw), the sharded 2-D transform's all-to-all layout; 31 = plain
+  int lsw = 31;
+  int64_t ss = 0;
 };
 
 bool use_fma(jwv_ctx* c) { return c->math == JWV_MATH_FMA; }
@@ -511,6 +516,7 @@ int store_pol_dir(int rev, bool final = false) { return rev && final ? 2 : 0; }
 Plan fwt_fwd_plan(jwv_ctx* c, const Bank& b, const Axis& a, int level, DevBuf* ws) {
   Plan p;
   const int nlev = fwd_levels(a.len, b.tw, level);
+  if (nlev == 0 && a.lsw < 31) return {};  // a copy into segments: the caller's pack
   if (nlev == 0) {
     p.push_back({false, 0, [c, a] { copy_axis(c, a); }});
     return p;
@@ -521,6 +527,13 @@ Plan fwt_fwd_plan(jwv_ctx* c, const Bank& b, const Axis& a, int level, DevBuf* w
   }
   const int C = col_slab(a.inner), cap = fwt_res_cap(C, a.outer), KM = Geo::fwt_k(C);
   const bool f1 = fast1(b, a, false);
+  const bool seg = a.lsw < 31;
+  const int sw = seg ? 1 << a.lsw : 0;
+  // segmented output: C = 1 tile kernels only, every tile's per-level detail
+  // range (T >> l <= T/2 samples, aligned) and every range written from the
+  // start of the row inside one segment; else an empty plan (the caller
+  // falls back to a plain pass + a pack)
+  if (seg && (!f1 || a.outer < 2 || sw < Geo::kFwt1T / 2)) return {};
   // levels of the tiled pass at level-input size h: KM, except that on the
   // fwt1 path the pass that ends the tiled part runs on down to kFwt1FwdTail
   // the first pass of one long signal may use its own tile / level count
@@ -571,13 +584,16 @@ Plan fwt_fwd_plan(jwv_ctx* c, const Bank& b, const Axis& a, int level, DevBuf* w
       return p;
     }
     const bool last = K == rem;
+    if (seg && last && (h >> K) > sw) return {};
     double* ad = last ? a.dst : ws[pp].p;
     const AxisView av = last ? a.dv : cview(h >> K, a.inner);
-    const jwv::TileArgs t{cur, cv, nullptr, {}, a.dst, a.dv, ad, av, h, K, a.outer, a.inner,
-                          dma_view(cur, cv, C, a.inner),
-                          Geo::tile_walk(),
-                          first1 && h == a.len && Geo::fwd1_first_t() != Geo::kFwt1T
-                              ? Geo::fwd1_first_t() : 0};
+    jwv::TileArgs t{cur, cv, nullptr, {}, a.dst, a.dv, ad, av, h, K, a.outer, a.inner,
+                    dma_view(cur, cv, C, a.inner),
+                    Geo::tile_walk(),
+                    first1 && h == a.len && Geo::fwd1_first_t() != Geo::kFwt1T
+                        ? Geo::fwd1_first_t() : 0};
+    t.lsw = a.lsw;
+    t.ss = a.ss;
     const int kind = h == a.len ? K_FWT_FWD_TILE : K_FWT_FWD_TILE_DEEP;
     const double bytes = 16.0 * a.outer * h * a.inner;
     p.push_back({false, 0, [c, &b, C, t, kind, bytes] {
@@ -591,6 +607,7 @@ Plan fwt_fwd_plan(jwv_ctx* c, const Bank& b, const Axis& a, int level, DevBuf* w
     pp ^= 1;
   }
   if (rem > 0) {
+    if (seg && h > sw) return {};
     const jwv::ResArgs r{cur, cv, a.dst, a.dv, h, 0, rem, a.outer, a.inner,
                          dma_view(cur, cv, C, a.inner)};
     const double bytes = 16.0 * a.outer * h * a.inner;
@@ -610,6 +627,7 @@ void fwt_fwd_axis(jwv_ctx* c, const Bank& b, const Axis& a, int level) {
 Plan fwt_rev_plan(jwv_ctx* c, const Bank& b, const Axis& a, int level, DevBuf* ws) {
   Plan p;
   const int h = rev_first(a.len, b.tw, level);
+  if (h == 0 && a.lsw < 31) return {};
   if (h == 0) {
     p.push_back({false, 0, [c, a] { copy_axis(c, a); }});
     return p;
@@ -622,6 +640,11 @@ Plan fwt_rev_plan(jwv_ctx* c, const Bank& b, const Axis& a, int level, DevBuf* w
   // fwt1 path, signal longer than one resident block: the resident tail stops
   // at kFwt1RevTail and the tiled passes take up to kFwt1KMax levels
   const bool f1 = fast1(b, a, true) && a.len > fwt_res_cap(C, a.outer);
+  // segmented input (see fwt_fwd_plan): C = 1 tiles, the resident part's
+  // prefix inside the first segment; else an empty plan
+  const bool seg = a.lsw < 31;
+  const int sw = seg ? 1 << a.lsw : 0;
+  if (seg && (!f1 || a.outer < 2)) return {};
   // batches of rows: the resident part stops at rev_row_tail(), one long
   // signal at kFwt1RevTail (the REV_HEAD plan)
   const int cap = f1 ? (a.outer > 1 ? rev_row_tail() : Geo::kFwt1RevTail) : Geo::res_cap(C);
@@ -670,6 +693,7 @@ Plan fwt_rev_plan(jwv_ctx* c, const Bank& b, const Axis& a, int level, DevBuf* w
     const int hres = std::min(a.len, cap);
     const int nres = exponent(hres / h) + 1;
     const bool last = hres == a.len;
+    if (seg && hres > sw) return {};
     double* out = last ? a.dst : ws[pp].p;
     const AxisView ov = last ? a.dv : cview(hres, a.inner);
     const jwv::ResArgs r{a.src, a.sv, out, ov, h, 0, nres, a.outer, a.inner,
@@ -685,6 +709,7 @@ Plan fwt_rev_plan(jwv_ctx* c, const Bank& b, const Axis& a, int level, DevBuf* w
     h1 = hres * 2;
     pp ^= 1;
   } else {
+    if (seg) return {};  // the first tile pass would read approximations from src
     acur = a.src;
     acv = a.sv;
     h1 = h;
@@ -695,10 +720,12 @@ Plan fwt_rev_plan(jwv_ctx* c, const Bank& b, const Axis& a, int level, DevBuf* w
     const bool last = hK == a.len;
     double* out = last ? a.dst : ws[pp].p;
     const AxisView ov = last ? a.dv : cview(hK, a.inner);
-    const jwv::TileArgs t{acur, acv, a.src, a.sv, out, ov, nullptr, {}, h1, K, a.outer, a.inner,
-                          dma_view(acur, acv, C, a.inner) && dma_view(a.src, a.sv, C, a.inner),
-                          (last ? store_pol_dir(1, a.outer == 1 && a.inner == 1) : 0) |
-                              Geo::tile_walk()};
+    jwv::TileArgs t{acur, acv, a.src, a.sv, out, ov, nullptr, {}, h1, K, a.outer, a.inner,
+                    dma_view(acur, acv, C, a.inner) && dma_view(a.src, a.sv, C, a.inner),
+                    (last ? store_pol_dir(1, a.outer == 1 && a.inner == 1) : 0) |
+                        Geo::tile_walk()};
+    t.lsw = a.lsw;
+    t.ss = a.ss;
     const int kind = last ? K_FWT_REV_TILE : K_FWT_REV_TILE_DEEP;
     const double bytes = 16.0 * a.outer * hK * a.inner;
     p.push_back({false, 0, [c, &b, C, t, kind, bytes] {
@@ -1330,6 +1357,7 @@ hipError_t launch_fwt_fwd_tile(const Bank& b, bool fma, int C, const TileArgs& a
   hipError_t e = hipSuccess;
   if (C == 1 && (fma ? fused::fwt_fwd_tile1(b, a, s, e) : exact::fwt_fwd_tile1(b, a, s, e)))
     return e;
+  if (a.lsw < 31) return hipErrorInvalidValue;  // segmented rows: C = 1 tiles only
   if (C == 8 && (fma ? fused::fwt_tile8(b, a, s, true, e) : exact::fwt_tile8(b, a, s, true, e)))
     return e;
   // the generic kernels are compiled for at most fwt_k(C) fused levels
@@ -1340,6 +1368,7 @@ hipError_t launch_fwt_rev_tile(const Bank& b, bool fma, int C, const TileArgs& a
   hipError_t e = hipSuccess;
   if (C == 1 && (fma ? fused::fwt_rev_tile1(b, a, s, e) : exact::fwt_rev_tile1(b, a, s, e)))
     return e;
+  if (a.lsw < 31) return hipErrorInvalidValue;  // segmented rows: C = 1 tiles only
   if (C == 8 && (fma ? fused::fwt_tile8(b, a, s, false, e) : exact::fwt_tile8(b, a, s, false, e)))
     return e;
   if (a.K > Geo::fwt_k(C)) return hipErrorInvalidValue;
@@ -1623,6 +1652,78 @@ JWV_BATCH(jwv_fwt_fwd_batch_f64, Kind::FWT, true)
 JWV_BATCH(jwv_fwt_rev_batch_f64, Kind::FWT, false)
 JWV_BATCH(jwv_wpt_fwd_batch_f64, Kind::WPT, true)
 JWV_BATCH(jwv_wpt_rev_batch_f64, Kind::WPT, false)
+
+// ---- segmented row passes (sharded 2-D transform) ----------------------------------
+// The row pass of BasicTransform.java:369-378 (forward) / :461-470 (reverse)
+// over a [rows][cols] block whose coefficient side is in the all-to-all layout
+// [cols/seg][rows][seg] (chunk j = columns [j seg, (j+1) seg) of every row),
+// so the sharded 2-D transform's exchange needs no pack / unpack pass
+// (jwave_amd/distributed.py).  Where the row kernels cannot address the
+// segments (short rows, seg < 1024, ...) the entry runs the plain row pass
+// and packs / unpacks with one copy.
+static void check_seg(int64_t rows, int64_t cols, int64_t seg) {
+  if (rows < 0 || cols < 0) throw Fail{JWV_ERR_BAD_CALL, "negative dimension"};
+  if (seg < 2 || (seg & (seg - 1)) || (cols && cols % seg) || seg > (int64_t(1) << 30))
+    throw Fail{JWV_ERR_BAD_CALL, "seg must be a power of two >= 2 dividing cols"};
+  if (rows * cols > (int64_t(1) << 33)) throw Fail{JWV_ERR_BAD_CALL, "matrix too large"};
+}
+// [rows][cols] view <-> [cols/seg][rows][seg] copy: outer = chunk, len = row
+static Axis seg_pack_axis(const double* plain, double* segd, int64_t rows, int64_t cols,
+                          int64_t seg, bool pack) {
+  AxisView pv{}, sv{};
+  pv.s_outer = seg; pv.s_len = cols; pv.pk = 1;
+  sv.s_outer = rows * seg; sv.s_len = seg; sv.pk = 1;
+  if (pack) return Axis{plain, pv, segd, sv, cols / seg, (int)rows, (int)seg};
+  return Axis{segd, sv, const_cast<double*>(plain), pv, cols / seg, (int)rows, (int)seg};
+}
+
+extern "C" int jwv_fwt_rows_seg_fwd_f64_dev(const double* x, double* y, int64_t rows,
+                                            int64_t cols, int level, int64_t seg,
+                                            const jwv_taps* t, jwv_ctx* c) {
+  return guarded(c, [&] {
+    const Bank b = make_bank(t);
+    check_seg(rows, cols, seg);
+    check_1d(Kind::FWT, true, cols, level);
+    if (rows == 0 || cols == 0) return;
+    need_device_ptrs(c, x, y);
+    check_overlap(x, (size_t)(rows * cols), y, (size_t)(rows * cols));
+    const AxisView rv = cview(cols, 1);
+    AxisView ov = rv;
+    ov.s_outer = seg;
+    Axis a{x, rv, y, ov, rows, (int)cols, 1};
+    a.lsw = exponent(seg);
+    a.ss = rows * seg;
+    Plan p = fwt_fwd_plan(c, b, a, level, c->ws);
+    if (!p.empty()) return run_plan(p);
+    double* tmp = grow(c, c->big, (size_t)(rows * cols));
+    fwt_fwd_axis(c, b, Axis{x, rv, tmp, rv, rows, (int)cols, 1}, level);
+    copy_axis(c, seg_pack_axis(tmp, y, rows, cols, seg, true));
+  });
+}
+
+extern "C" int jwv_fwt_rows_seg_rev_f64_dev(const double* y, double* x, int64_t rows,
+                                            int64_t cols, int level, int64_t seg,
+                                            const jwv_taps* t, jwv_ctx* c) {
+  return guarded(c, [&] {
+    const Bank b = make_bank(t);
+    check_seg(rows, cols, seg);
+    check_1d(Kind::FWT, false, cols, level);
+    if (rows == 0 || cols == 0) return;
+    need_device_ptrs(c, y, x);
+    check_overlap(y, (size_t)(rows * cols), x, (size_t)(rows * cols));
+    const AxisView rv = cview(cols, 1);
+    AxisView iv = rv;
+    iv.s_outer = seg;
+    Axis a{y, iv, x, rv, rows, (int)cols, 1};
+    a.lsw = exponent(seg);
+    a.ss = rows * seg;
+    Plan p = fwt_rev_plan(c, b, a, level, c->ws);
+    if (!p.empty()) return run_plan(p);
+    double* tmp = grow(c, c->big, (size_t)(rows * cols));
+    copy_axis(c, seg_pack_axis(tmp, const_cast<double*>(y), rows, cols, seg, false));
+    fwt_rev_axis(c, b, Axis{tmp, rv, x, rv, rows, (int)cols, 1}, level);
+  });
+}
 
 // ---- 2-D / 3-D -------------------------------------------------------------------
 static void check_2d(Kind k, bool fwd, int64_t rows, int64_t cols, int lvl_m, int lvl_n) {

@@ -50,9 +50,15 @@ struct Fwd1Level {
   // yd0: the signal's coefficient row; ya: its level-K approximation row.
   // Each lane computes two adjacent pairs (p, p+1): one 16-B store per lane
   // for the details and approximations, L+2 window reads for two pairs.
+  // Segmented rows (lsw < 31): sample i of the row lives at
+  // yd0 + (i >> lsw) * ss + (i & (2^lsw - 1)) -- the [W][rows][cols/W] send
+  // layout of the sharded 2-D transform (distributed.py); a level's detail
+  // range of one tile (T >> l samples, aligned) never straddles a segment
+  // (host: 2^lsw >= T / 2).
   __device__ __forceinline__ static void run(const FwdTaps<L>& tp, double* lds,
                                              double* __restrict__ yd0, int hl, int t,
-                                             double* __restrict__ ya, int sp = 0) {
+                                             double* __restrict__ ya, int sp = 0, int lsw = 31,
+                                             int64_t ss = 0) {
     using G = Fwd1Geo<L, T, K>;
     JWV_STAMP(10 + l);
     constexpr int mo = G::m(l);      // even
@@ -62,7 +68,9 @@ struct Fwd1Level {
     const double* in = lds + (l == 1 ? 0 : G::off(l - 1));
     double* out = lds + G::off(l);
     const int tid = opaque_tid();  // per-level: keeps address math out of the prologue
-    double* __restrict__ yd = yd0 + (hl >> 1) + (int64_t)t * own;
+    const int i0 = (hl >> 1) + t * own;
+    double* __restrict__ yd =
+        yd0 + (int64_t)(i0 >> lsw) * ss + (i0 & (int)((1u << (lsw & 31)) - 1u));
     double2 av[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -109,7 +117,7 @@ struct Fwd1Level {
         }
       }
       lds_barrier();
-      Fwd1Level<L, NT, T, K, FMA, l + 1, WT>::run(tp, lds, yd0, hl >> 1, t, ya, sp);
+      Fwd1Level<L, NT, T, K, FMA, l + 1, WT>::run(tp, lds, yd0, hl >> 1, t, ya, sp, lsw, ss);
     }
   }
 };
@@ -122,7 +130,7 @@ __global__ __launch_bounds__(NT) void fwt_fwd_tile1(const double* __restrict__ s
                                                     int64_t s_src, double* __restrict__ dst,
                                                     int64_t s_dst, double* __restrict__ adst,
                                                     int64_t s_adst, int h, FwdTaps<L> tp,
-                                                    int sp) {
+                                                    int sp, int lsw, int64_t ss) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   using G = Fwd1Geo<L, T, K>;
   constexpr int M0 = G::m(0);
@@ -138,7 +146,7 @@ __global__ __launch_bounds__(NT) void fwt_fwd_tile1(const double* __restrict__ s
   dma_fence_barrier();
   JWV_STAMP(1);
   Fwd1Level<L, NT, T, K, FMA, 1, false>::run(tp, lds, dst + o * s_dst, h, t, adst + o * s_adst,
-                                                 sp);
+                                                 sp, lsw, ss);
 }
 
 // ---------------------------------------------------------------- reverse
@@ -351,7 +359,7 @@ __global__ __launch_bounds__(NT) void fwt_rev_tile1(const double* __restrict__ a
                                                     int64_t s_a, const double* __restrict__ coef,
                                                     int64_t s_c, double* __restrict__ dst,
                                                     int64_t s_d, int hK, RevTaps<L> tp,
-                                                    int sp) {
+                                                    int sp, int lsw, int64_t ss) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   using G = Rev1Geo<L, T, K>;
   constexpr int MAXU = (G::len(1) + NT - 1) / NT;
@@ -372,8 +380,14 @@ __global__ __launch_bounds__(NT) void fwt_rev_tile1(const double* __restrict__ a
   for (int l = K - 1; l >= 0; --l) {
     const int half = hK >> (l + 1), hm = half - 1;
     const int B = (t * T >> (l + 1)) - G::c(l + 1);
+    // segmented coefficient rows (lsw < 31, see Fwd1Level): a 16-B piece
+    // (e even, segments of even length) never straddles a segment
+    const int sm = (int)((1u << (lsw & 31)) - 1u);
     load_window<1, NT, MAXU>(lds + (IP ? G::ip_doff(l) : G::doff(l)), sc, G::len(l + 1), true, 0,
-                             1, [&](int e) { return (int64_t)half + ((B + e) & hm); });
+                             1, [&](int e) {
+                               const int i = half + ((B + e) & hm);
+                               return (int64_t)(i >> lsw) * ss + (i & sm);
+                             });
   }
   dma_fence_barrier();
   Rev1Level<L, NT, T, K, FMA, K - 1, false, true, IP>::run(tp, lds, t, dst + o * s_d, sp);

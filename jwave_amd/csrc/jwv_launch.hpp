@@ -71,6 +71,10 @@ struct TileArgs {  // tiled FWT/WPT kernels
   int dma;
   int sp = 0;  // cache policy of the full-length output stores (st2_pol), C = 1 kernels
   int t1 = 0;  // C = 1 forward tile: 0 = Geo::kFwt1T, or 1024 (first pass of a long signal)
+  // C = 1 tiles: segmented rows of the coefficient array (forward dst /
+  // reverse coef): sample i at row + (i >> lsw) * ss + (i mod 2^lsw); 31 = plain
+  int lsw = 31;
+  int64_t ss = 0;
 };
 // AncientEgyptianDecomposition varlen launch (aed_kernels.hpp): contiguous
 // 1-D segments of src / dst, one block each.

@@ -40,7 +40,7 @@ hipError_t fwd1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
   for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
   const dim3 grid((unsigned)(a.nouter * (a.h / T)));
   JWV_LAUNCH(k, grid, dim3(NT), lds, s, a.src, a.sv.s_outer, a.dst, a.dv.s_outer, a.adst,
-                     a.av.s_outer, a.h, tp, a.sp);
+                     a.av.s_outer, a.h, tp, a.sp, a.lsw, a.ss);
   return hipGetLastError();
 }
 template <int L>
@@ -80,7 +80,7 @@ hipError_t rev1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
   const int hK = a.h << (a.K - 1);
   const dim3 grid((unsigned)(a.nouter * (hK / T)));
   JWV_LAUNCH(k, grid, dim3(NT), lds, s, a.src, a.sv.s_outer, a.coef, a.cv.s_outer, a.dst,
-                     a.dv.s_outer, hK, tp, a.sp);
+                     a.dv.s_outer, hK, tp, a.sp, a.lsw, a.ss);
   return hipGetLastError();
 }
 template <int L>

@@ -7,7 +7,9 @@ What shards, and how:
   no data-path collective (`shard_range`, `batch_forward/reverse`).
 * 2-D FWT (config 3, BasicTransform.java:361-474): row block per rank -> row
   pass -> all-to-all transpose of [R/W x C/W] blocks -> column pass on the
-  [R][C/W] slab.  The forward result stays in that column-slab layout, which
+  [R][C/W] slab.  The row kernels write (forward) / read (reverse) the
+  all-to-all chunk layout directly (jwv_fwt_rows_seg_*), so no pack / unpack
+  pass touches HBM around the exchange.  The forward result stays in that column-slab layout, which
   is exactly what the sharded reverse consumes; `gather_cols` assembles it.
 * MODWT of one long signal (config 5, MODWTTransform.java:256-375): contiguous
   slices; forward receives a left halo of H = (L-1)(2^J - 1) samples from its
@@ -50,6 +52,14 @@ class HipBackend:
     def cols(self, x, w, level, forward, kind="fwt"):
         # [R][cw] slab: transform along dim 0 (outer = 1, inner = cw)
         return T.transform_axis(x, w, level, 0, forward, self.ctx, kind=kind)
+
+    def rows_to_chunks(self, x, w, level, seg):
+        """FWT row pass writing the all-to-all send layout [C/seg][rw][seg]."""
+        return T.fwt_rows_to_chunks(x, w, level, seg, self.ctx)
+
+    def chunks_to_rows(self, y, w, level):
+        """FWT reverse row pass reading the all-to-all receive layout."""
+        return T.fwt_chunks_to_rows(y, w, level, self.ctx)
 
     def modwt_fwd(self, x, w, J):
         return T.modwt_forward(x, w, J, self.ctx)
@@ -101,46 +111,57 @@ def _check_2d(rows, cols, W):
                          "(%d x %d over %d ranks)" % (rows, cols, W))
 
 
-def _transpose_rows_to_cols(a, W, group):
-    """[rw][C] row block -> [R][cw] column slab (all-to-all of [rw][cw] blocks)."""
-    rw, C = a.shape
+def _rows_to_send(x_rows, w, level, W, backend, kind):
+    """Row pass whose result is the all-to-all send buffer [W][rw][cw] (chunk
+    j -> rank j).  A backend with rows_to_chunks (HipBackend, FWT) writes
+    that layout from the row kernels; otherwise the plain rows are packed
+    with one copy."""
+    rw, C = x_rows.shape
     cw = C // W
-    send = a.reshape(rw, W, cw).permute(1, 0, 2).contiguous()  # [W][rw][cw], chunk j -> rank j
-    recv = torch.empty_like(send)                              # chunk i <- rank i's rows
-    dist.all_to_all_single(recv, send, group=group)
-    return recv.reshape(W * rw, cw)
+    if kind == "fwt" and hasattr(backend, "rows_to_chunks"):
+        return backend.rows_to_chunks(x_rows, w, level, cw)
+    a = backend.rows(x_rows, w, level, True, kind)
+    return a.reshape(rw, W, cw).permute(1, 0, 2).contiguous()
 
 
-def _transpose_cols_to_rows(b, W, group):
-    """[R][cw] column slab -> [rw][C] row block (inverse of the above)."""
-    R, cw = b.shape
-    rw = R // W
-    send = b.reshape(W, rw, cw).contiguous()   # chunk i = rows of rank i
-    recv = torch.empty_like(send)              # chunk j = my rows of rank j's columns
+def _recv_to_rows(recv, w, level, backend, kind):
+    """Reverse row pass reading the all-to-all receive buffer [W][rw][cw]
+    (chunk j = my rows of rank j's columns) in place where the backend can."""
+    W, rw, cw = recv.shape
+    if kind == "fwt" and hasattr(backend, "chunks_to_rows"):
+        return backend.chunks_to_rows(recv, w, level)
+    return backend.rows(recv.permute(1, 0, 2).reshape(rw, W * cw), w, level, False, kind)
+
+
+def _exchange(send, group):
+    """all-to-all of the [W][rw][cw] chunks: chunk j -> rank j, chunk i <- rank i."""
+    recv = torch.empty_like(send)
     dist.all_to_all_single(recv, send, group=group)
-    return recv.permute(1, 0, 2).reshape(rw, W * cw)
+    return recv
 
 
 def forward_2d(x_rows, rows, cols, w, lvl_m, lvl_n, backend, group=None, kind="fwt"):
     """BasicTransform.forward(double[][], lvlM, lvlN) (BasicTransform.java:361-399)
     sharded: x_rows = this rank's [rows/W][cols] block; returns this rank's
-    [rows][cols/W] column slab of the result."""
+    [rows][cols/W] column slab of the result.  HBM passes per rank besides the
+    two transforms: none -- the row pass writes the send chunks, the column
+    pass reads the receive buffer as the [rows][cols/W] slab it is."""
     W, _ = _world(group)
     _check_2d(rows, cols, W)
-    a = backend.rows(x_rows, w, lvl_n, True, kind)
-    b = _transpose_rows_to_cols(a, W, group)
-    return backend.cols(b, w, lvl_m, True, kind)
+    recv = _exchange(_rows_to_send(x_rows, w, lvl_n, W, backend, kind), group)
+    return backend.cols(recv.reshape(rows, cols // W), w, lvl_m, True, kind)
 
 
 def reverse_2d(y_cols, rows, cols, w, lvl_m, lvl_n, backend, group=None, kind="fwt"):
     """BasicTransform.reverse(double[][], lvlM, lvlN) (BasicTransform.java:436-474)
     sharded: y_cols = this rank's [rows][cols/W] slab; returns its
-    [rows/W][cols] row block of the reconstruction."""
+    [rows/W][cols] row block of the reconstruction.  The column pass's output
+    is the send buffer as is; the row pass reads the receive chunks."""
     W, _ = _world(group)
     _check_2d(rows, cols, W)
     b = backend.cols(y_cols, w, lvl_m, False, kind)
-    a = _transpose_cols_to_rows(b, W, group)
-    return backend.rows(a, w, lvl_n, False, kind)
+    recv = _exchange(b.reshape(W, rows // W, cols // W), group)
+    return _recv_to_rows(recv, w, lvl_n, backend, kind)
 
 
 def gather_cols(slab, group=None):

@@ -353,6 +353,32 @@ def transform_axis(x, wavelet, level, axis_len_dim=1, forward=True, ctx=None, ki
                 (outer, ln, inner, int(level), _TapsHolder.of(wavelet)))
 
 
+def fwt_rows_to_chunks(x, wavelet, level, seg, ctx=None):
+    """Forward FWT of every row of the device matrix x [rows][cols], result in
+    the sharded 2-D transform's all-to-all layout [cols/seg][rows][seg]
+    (chunk j = columns [j seg, (j+1) seg)); jwv_fwt_rows_seg_fwd_f64_dev.
+    Values are those of fwt_forward(x) (BasicTransform.java:369-378)."""
+    if not (_is_torch(x) and x.is_cuda and x.dim() == 2):
+        raise JWaveError("fwt_rows_to_chunks takes a [rows][cols] float64 device tensor")
+    rows, cols = (int(v) for v in x.shape)
+    seg = int(seg)
+    if seg < 1 or cols % seg:
+        raise JWaveError("fwt_rows_to_chunks: seg must divide cols (%d, %d)" % (seg, cols))
+    return _run(None, "jwv_fwt_rows_seg_fwd_f64_dev", ctx, x, (cols // seg, rows, seg),
+                (rows, cols, int(level), seg, _TapsHolder.of(wavelet)))
+
+
+def fwt_chunks_to_rows(y, wavelet, level, ctx=None):
+    """Reverse of fwt_rows_to_chunks: y [cols/seg][rows][seg] (chunked
+    coefficient rows) -> [rows][cols]; jwv_fwt_rows_seg_rev_f64_dev.  Values
+    are those of fwt_reverse on the plain rows (BasicTransform.java:461-470)."""
+    if not (_is_torch(y) and y.is_cuda and y.dim() == 3):
+        raise JWaveError("fwt_chunks_to_rows takes a [chunks][rows][seg] float64 device tensor")
+    nch, rows, seg = (int(v) for v in y.shape)
+    return _run(None, "jwv_fwt_rows_seg_rev_f64_dev", ctx, y, (rows, nch * seg),
+                (rows, nch * seg, int(level), seg, _TapsHolder.of(wavelet)))
+
+
 def modwt_forward(x, wavelet, J, ctx=None):
     if not _is_torch(x):
         x = np.ascontiguousarray(np.asarray(x, dtype=np.float64))

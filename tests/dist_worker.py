@@ -47,6 +47,23 @@ class OracleBackend:
             c[:, col0:col0 + n].numpy())))
 
 
+class ChunkedOracleBackend(OracleBackend):
+    """OracleBackend plus the chunked row passes HipBackend has (the oracle's
+    rows, laid out as jwv_fwt_rows_seg_* lay them out: [cols/seg][rows][seg]),
+    so the gloo runs exercise the exchange without pack / unpack copies."""
+
+    def rows_to_chunks(self, x, w, level, seg):
+        y = oracle.batch("fwt", True, w, x.numpy(), level)
+        rows, cols = y.shape
+        return torch.from_numpy(np.ascontiguousarray(
+            y.reshape(rows, cols // seg, seg).transpose(1, 0, 2)))
+
+    def chunks_to_rows(self, y, w, level):
+        nch, rows, seg = y.shape
+        plain = np.ascontiguousarray(y.numpy().transpose(1, 0, 2).reshape(rows, nch * seg))
+        return torch.from_numpy(oracle.batch("fwt", False, w, plain, level))
+
+
 def same(a, b, what):
     a = a.detach().cpu().numpy() if torch.is_tensor(a) else a
     if a.shape != b.shape or not np.array_equal(a, b):
@@ -88,20 +105,26 @@ def main():
                                                     oracle.batch(kind, True, w, full, lev), lev),
              "%s batch rev" % kind)
 
-    # ---- 2-D: row pass, all-to-all transpose, column pass
-    for wname, rows, cols, lm, ln in (("Daubechies8", 64, 128, 6, 7), ("Haar1", 32, 16, 2, 3),
-                                      ("Daubechies4", 128, 64, 5, 0)):
+    # ---- 2-D: row pass, all-to-all transpose, column pass (FWT: chunked row
+    # passes and, on gloo, also the packing fallback; WPT: the fallback)
+    bes2 = [be] if a.backend == "nccl" else [ChunkedOracleBackend(), be]
+    for kind, wname, rows, cols, lm, ln in (
+            ("fwt", "Daubechies8", 64, 128, 6, 7), ("fwt", "Haar1", 32, 16, 2, 3),
+            ("fwt", "Daubechies4", 128, 64, 5, 0), ("fwt", "Daubechies4", 8, 4096, 3, 12),
+            ("wpt", "Symlet8", 64, 64, 4, 5)):
         if rows % W or cols % W:
             continue
         w = jw.by_class(wname)
         full = oracle.java_random_doubles(123456789, rows * cols).reshape(rows, cols)
         rw = rows // W
-        yc = D.forward_2d(put(full[r * rw:(r + 1) * rw]), rows, cols, w, lm, ln, be)
-        ref = oracle.transform_2d("fwt", True, w, full, lm, ln)
-        same(D.gather_cols(yc), ref, "2d fwd %s" % wname)
-        xr = D.reverse_2d(yc, rows, cols, w, lm, ln, be)
-        same(D.gather_rows(xr, rows), oracle.transform_2d("fwt", False, w, ref, lm, ln),
-             "2d rev %s" % wname)
+        ref = oracle.transform_2d(kind, True, w, full, lm, ln)
+        for b2 in bes2:
+            tag = "%s %s %dx%d %s" % (kind, wname, rows, cols, type(b2).__name__)
+            yc = D.forward_2d(put(full[r * rw:(r + 1) * rw]), rows, cols, w, lm, ln, b2, kind=kind)
+            same(D.gather_cols(yc), ref, "2d fwd " + tag)
+            xr = D.reverse_2d(yc, rows, cols, w, lm, ln, b2, kind=kind)
+            same(D.gather_rows(xr, rows), oracle.transform_2d(kind, False, w, ref, lm, ln),
+                 "2d rev " + tag)
 
     # ---- MODWT of one long signal: ring halo exchange
     for wname, n, J in (("Daubechies4", 1000, 5), ("Haar1", 1001, 3), ("Daubechies8", 4096, 4)):

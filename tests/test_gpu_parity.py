@@ -345,6 +345,69 @@ def test_fwt2d_overlapped_schedule(ctx, ctx_fma, wname, shape):
             assert_close(T.transform_2d(yr, w, lm, ln, False, ctx_fma), xr, "2d rev fma")
 
 
+@pytest.mark.parametrize("wname", ["Haar1", "Daubechies4", "Daubechies8", "Symlet8", "Coiflet1",
+                                   "BiOrthogonal35", "Daubechies20"])
+@pytest.mark.parametrize("shape", [(64, 8192, 1024), (32, 8192, 2048), (16, 65536, 8192),
+                                   (8, 4096, 4096), (64, 16384, 16384), (8, 8192, 512),
+                                   (3, 2048, 256), (1, 8192, 1024), (40, 32768, 1024)])
+def test_fwt_rows_chunked(ctx, ctx_fma, wname, shape):
+    """jwv_fwt_rows_seg_{fwd,rev}_f64_dev (the sharded 2-D transform's row
+    passes): values of the plain batched row FWT, laid out [cols/seg][rows][seg].
+    seg >= 1024 with >= 2 rows on the fast banks runs the row kernels with
+    chunked addressing (no copy launch); short chunks, one row and the generic
+    banks take the plain pass + one packing copy (as do partial levels whose
+    approximation prefix outgrows the first chunk).  Full and partial levels."""
+    import torch
+    w = jw.by_class(wname)
+    rows, cols, seg = shape
+    x = rnd(rows * cols, rows + 5 * cols + seg).reshape(rows, cols)
+    xd = torch.from_numpy(x).cuda()
+    full = cols.bit_length() - 1
+    fast = wname in ("Haar1", "Daubechies4", "Daubechies8", "Symlet8")  # static-L banks
+
+    def chunk(a):
+        return np.ascontiguousarray(a.reshape(rows, cols // seg, seg).transpose(1, 0, 2))
+
+    for lev in sorted({0, 1, 5, full - 3, full}):
+        yr = oracle.batch("fwt", True, w, x, lev)
+        ctx.profile(True)
+        y = T.fwt_rows_to_chunks(xd, w, lev, seg, ctx)
+        prof = ctx.profile_read()
+        ctx.profile(False)
+        assert tuple(y.shape) == (cols // seg, rows, seg)
+        assert_exact(y.cpu().numpy(), chunk(yr), "seg fwd %s %s l=%d" % (wname, shape, lev))
+        if fast and rows >= 2 and seg >= 1024 and lev == full and cols > 8192:
+            assert "copy_axis" not in prof, "seg fwd packed with a copy: %s" % sorted(prof)
+        xr = oracle.batch("fwt", False, w, yr, lev)
+        yd = torch.from_numpy(chunk(yr)).cuda()
+        ctx.profile(True)
+        got = T.fwt_chunks_to_rows(yd, w, lev, ctx)
+        prof = ctx.profile_read()
+        ctx.profile(False)
+        assert_exact(got.cpu().numpy(), xr, "seg rev %s %s l=%d" % (wname, shape, lev))
+        if fast and rows >= 2 and seg >= 1024 and lev == full and cols > 8192:
+            assert "copy_axis" not in prof, "seg rev unpacked with a copy: %s" % sorted(prof)
+        if lev == full and wname == "Daubechies8":
+            assert_close(T.fwt_rows_to_chunks(xd, w, lev, seg, ctx_fma).cpu().numpy(), chunk(yr),
+                         "seg fwd fma")
+            assert_close(T.fwt_chunks_to_rows(yd, w, lev, ctx_fma).cpu().numpy(), xr,
+                         "seg rev fma")
+
+
+def test_fwt_rows_chunked_errors(ctx):
+    import torch
+    w = jw.by_class("Daubechies4")
+    xd = torch.zeros((4, 4096), dtype=torch.float64, device="cuda")
+    with pytest.raises(jw.JWaveError):
+        T.fwt_rows_to_chunks(xd, w, 12, 1, ctx)           # seg < 2
+    with pytest.raises(jw.JWaveError):
+        T.fwt_rows_to_chunks(xd, w, 12, 3000, ctx)        # does not divide cols
+    with pytest.raises(jw.JWaveError):
+        T.fwt_rows_to_chunks(xd[:, :3000].contiguous(), w, 3, 1000, ctx)  # not 2^p
+    with pytest.raises(jw.JWaveFailure, match="level is out of range"):
+        T.fwt_rows_to_chunks(xd, w, 13, 1024, ctx)        # the reference's own check
+
+
 @pytest.mark.parametrize("wname", ["Haar1", "Daubechies2", "Daubechies4", "Daubechies8", "Symlet8"])
 def test_fwt_batch_rowcap(ctx, wname):
     """Batched 1-D FWT, 64 signals x 8192 (>= 64 rows, > 2048 samples: the
