@@ -22,6 +22,17 @@
 #pragma once
 #include "fwt1_kernels.hpp"
 
+// JWV_WPT_UDIV: slot -> (window, pair) by unsigned division (the signed
+// form costs a sign fix-up per slot).  JWV_WPT_HEADOVR: the reverse stores
+// every couple unpredicated; in the head tiles the array-head lanes rewrite
+// their pairs after one extra barrier.
+#ifndef JWV_WPT_UDIV
+#define JWV_WPT_UDIV 1
+#endif
+#ifndef JWV_WPT_HEADOVR
+#define JWV_WPT_HEADOVR 1
+#endif
+
 namespace jwv {
 
 // ---------------------------------------------------------------- forward
@@ -48,7 +59,12 @@ struct Wpt1FwdLevel {
     for (int r = 0; r < R; ++r) {
       const int q = tid + r * NT;
       if ((r + 1) * NT <= NC || q < NC) {
+#if JWV_WPT_UDIV
+        const int s = (int)((unsigned)q / (unsigned)(mo / 2));       // sub-window
+        const int i = (int)(2u * ((unsigned)q % (unsigned)(mo / 2)));  // first pair
+#else
         const int s = q / (mo / 2), i = 2 * (q % (mo / 2));  // sub-window, first pair
+#endif
         wo[r] = (2 * s) * mo + i;
         const double* in = lds + s * mi + 2 * i;
         double x[L + 2];
@@ -192,7 +208,12 @@ struct Wpt1RevLevel {
     for (int r = 0; r < R; ++r) {
       const int k = tid + r * NT;
       if ((r + 1) * NT <= NC || k < NC) {
+#if JWV_WPT_UDIV
+        const int s = (int)((unsigned)k / (unsigned)NCW);
+        const int ml = (int)(2u * ((unsigned)k % (unsigned)NCW));
+#else
         const int s = k / NCW, ml = 2 * (k % NCW);
+#endif
         const double* ab = lds + (2 * s) * li_;
         const double* db = ab + li_;
         const int st = off + ml - (Q - 1) - sh;  // even
@@ -221,10 +242,17 @@ struct Wpt1RevLevel {
           rev_pair<L, FMA>(tp, av + Q + sh, dv + Q + sh, 1, x1e, x1o);
         }
         asm volatile("" : "+v"(x0e), "+v"(x0o), "+v"(x1e), "+v"(x1o) :: "memory");  // slot boundary
+#if JWV_WPT_HEADOVR
+        // array-head pairs are stored like the others and overwritten by the
+        // head lanes after one more barrier (head tiles only, below)
+        const bool w0 = true;
+        const bool w1 = (NPW % 2 == 0) || ml + 1 < NPW;
+#else
         const int mg = pbase + ml;
         const bool w0 = !(head_tile && mg >= 0 && mg < Q - 1);
         const bool w1 = ((NPW % 2 == 0) || ml + 1 < NPW) &&
                         !(head_tile && mg + 1 >= 0 && mg + 1 < Q - 1);
+#endif
         if constexpr (l == 1) {
           double* yo = y + (int64_t)t * T + 2 * ml;
           if (w0) *reinterpret_cast<double2*>(yo) = make_double2(x0e, x0o);
@@ -251,7 +279,14 @@ struct Wpt1RevLevel {
       }
     }
     if constexpr (l == 1) {
+#if JWV_WPT_HEADOVR
+      if (head_tile) {
+        __syncthreads();  // the couples' stores of the head pairs first (workgroup order)
+        if (hs >= 0) *reinterpret_cast<double2*>(y + (int64_t)t * T + 2 * hml) = make_double2(hxe, hxo);
+      }
+#else
       if (hs >= 0) *reinterpret_cast<double2*>(y + (int64_t)t * T + 2 * hml) = make_double2(hxe, hxo);
+#endif
     } else {
       lds_barrier();
 #pragma unroll
@@ -263,7 +298,14 @@ struct Wpt1RevLevel {
           if (wo[r] & 2) *reinterpret_cast<double2*>(ob + 2) = make_double2(rx[r].z, rx[r].w);
         }
       }
+#if JWV_WPT_HEADOVR
+      if (head_tile) {
+        lds_barrier();
+        if (hs >= 0) *reinterpret_cast<double2*>(lds + hs * lo_ + 2 * hml) = make_double2(hxe, hxo);
+      }
+#else
       if (hs >= 0) *reinterpret_cast<double2*>(lds + hs * lo_ + 2 * hml) = make_double2(hxe, hxo);
+#endif
       lds_barrier();
       Wpt1RevLevel<L, NT, T, K, FMA, l - 1, ILV>::run(tp, lds, t, y);
     }
