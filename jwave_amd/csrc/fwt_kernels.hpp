@@ -98,12 +98,23 @@ __device__ __forceinline__ void fwd_pair(const typename FB<L>::Fwd& tp, At at, d
 #ifndef JWV_WPT_RPIPE
 #define JWV_WPT_RPIPE 2
 #endif
+// ZS = false ("no zero start", EXACT only): a sum starts at its first
+// product instead of adding it to +0.0.  The two folds differ only in the
+// sign of a zero running sum (start +0.0: never -0 under round-to-nearest;
+// first product: possibly -0), so every non-zero value is identical and a
+// -0 can only stand where Java holds +0.  Products of such a zero are zeros
+// again, so the same holds for every later level fed from it, and a level
+// that starts from +0.0 (ZS = true) restores Java's sign.  Used for the WPT
+// tiles' LDS-only levels; the level that writes HBM keeps ZS = true.
+#ifndef JWV_WPT_NZS
+#define JWV_WPT_NZS 1
+#endif
 // A couple's four sums (pairs at x and x + 2, analysis lo / hi) with the
 // products of G taps issued ahead of their adds: per group 4G independent
 // multiplies, then the 4G adds in the per-output order (j ascending), so no
 // add waits on the multiply issued just before it and the four chains
 // alternate.  Same operations and order per output as fwd_pair (bit-exact).
-template <int L, bool FMA, int G>
+template <int L, bool FMA, int G, bool ZS = true>
 __device__ __forceinline__ void fwd_couple_pipe(const FwdTaps<L>& tp, const double* x,
                                                 double& a0, double& d0, double& a1, double& d1) {
   static_assert(L % G == 0, "tap groups");
@@ -127,6 +138,11 @@ __device__ __forceinline__ void fwd_couple_pipe(const FwdTaps<L>& tp, const doub
         sd0 = __builtin_fma(x[j0 + g], tp.hi[j0 + g], sd0);
         sa1 = __builtin_fma(x[j0 + g + 2], tp.lo[j0 + g], sa1);
         sd1 = __builtin_fma(x[j0 + g + 2], tp.hi[j0 + g], sd1);
+      } else if (!ZS && j0 == 0 && g == 0) {
+        sa0 = pa0[0];
+        sd0 = pd0[0];
+        sa1 = pa1[0];
+        sd1 = pd1[0];
       } else {
         sa0 = sa0 + pa0[g];
         sd0 = sd0 + pd0[g];
@@ -147,8 +163,8 @@ __device__ __forceinline__ void fwd_couple_pipe(const FwdTaps<L>& tp, const doub
 // per group 8G independent multiplies (a*lor, d*hir of both pairs, even and
 // odd outputs), then the 4G term sums a*lor + d*hir, then the 4G accumulator
 // adds; each output keeps its order (q descending) and its operations
-// (EXACT only; bit-exact with rev_pair / rev_couple_ilv).
-template <int L, int G>
+// (EXACT only; bit-exact with rev_pair / rev_couple_ilv; ZS as above).
+template <int L, int G, bool ZS = true>
 __device__ __forceinline__ void rev_couple_pipe(const RevTaps<L>& tp, const double* A,
                                                 const double* D, double& e0, double& o0,
                                                 double& e1, double& o1) {
@@ -186,10 +202,17 @@ __device__ __forceinline__ void rev_couple_pipe(const RevTaps<L>& tp, const doub
     }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      se0 += ve0[g];
-      se1 += ve1[g];
-      so0 += vo0[g];
-      so1 += vo1[g];
+      if (!ZS && q0 == Q - 1 && g == 0) {
+        se0 = ve0[0];
+        se1 = ve1[0];
+        so0 = vo0[0];
+        so1 = vo1[0];
+      } else {
+        se0 += ve0[g];
+        se1 += ve1[g];
+        so0 += vo0[g];
+        so1 += vo1[g];
+      }
     }
     asm volatile("" : "+v"(se0), "+v"(so0), "+v"(se1), "+v"(so1));
   }

@@ -76,7 +76,8 @@ struct Wpt1FwdLevel {
         }
         double a0, d0, a1, d1;
         if constexpr (JWV_WPT_FPIPE > 0 && !FMA) {
-          fwd_couple_pipe<L, FMA, (JWV_WPT_FPIPE < L ? JWV_WPT_FPIPE : L)>(tp, x, a0, d0, a1, d1);
+          fwd_couple_pipe<L, FMA, (JWV_WPT_FPIPE < L ? JWV_WPT_FPIPE : L), !JWV_WPT_NZS || l == K>(
+              tp, x, a0, d0, a1, d1);
         } else {
           fwd_pair<L, FMA>(tp, [&](int j) { return x[j]; }, a0, d0);
           fwd_pair<L, FMA>(tp, [&](int j) { return x[j + 2]; }, a1, d1);
@@ -233,7 +234,7 @@ struct Wpt1RevLevel {
         // pair ml: a[li - q] = av[(Q-1) + sh - q]; pair ml+1: one further
         double x0e, x0o, x1e, x1o;
         if constexpr (ILV && !FMA && JWV_WPT_RPIPE > 0 && (L / 2) % JWV_WPT_RPIPE == 0) {
-          rev_couple_pipe<L, JWV_WPT_RPIPE>(tp, av + (Q - 1) + sh, dv + (Q - 1) + sh, x0e, x0o,
+          rev_couple_pipe<L, JWV_WPT_RPIPE, !JWV_WPT_NZS || l == 1>(tp, av + (Q - 1) + sh, dv + (Q - 1) + sh, x0e, x0o,
                                             x1e, x1o);
         } else if constexpr (ILV) {
           rev_couple_ilv<L, FMA>(tp, av + (Q - 1) + sh, dv + (Q - 1) + sh, x0e, x0o, x1e, x1o);

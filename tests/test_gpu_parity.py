@@ -235,6 +235,43 @@ def test_wpt_config4_shape(ctx, ctx_fma):
     assert_close(T.wpt_reverse(yr, w, 6, ctx_fma), xr_ref, "wpt cfg4 rev fma")
 
 
+def assert_bits(got, ref, what=""):
+    """Bit-for-bit, signed zeros included (np.array_equal has -0.0 == +0.0)."""
+    got = np.ascontiguousarray(np.asarray(got, dtype=np.float64))
+    ref = np.ascontiguousarray(ref)
+    gb, rb = got.view(np.int64), ref.view(np.int64)
+    bad = np.flatnonzero(gb != rb)
+    assert bad.size == 0, "%s: %d values differ in their bits, first at %d (got %r ref %r)" % (
+        what, bad.size, bad[0], got.flat[bad[0]], ref.flat[bad[0]])
+
+
+@pytest.mark.parametrize("wname", ["Symlet8", "Daubechies4", "Haar1", "Coiflet1", "Daubechies8"])
+def test_wpt_signed_zeros(ctx, wname):
+    """The WPT tiles' LDS-only levels start each sum at its first product
+    (fwt_kernels.hpp, ZS): values identical, a zero's sign possibly not, until
+    the level that writes HBM starts from +0.0 again.  Inputs with runs of
+    +0.0 / -0.0 and isolated values make many outputs exact zeros of both
+    product signs; every output must match Java's bits, zero signs included."""
+    w = jw.by_class(wname)
+    rng = np.random.default_rng(7)
+    n, B = 1 << 16, 3
+    x = np.stack([rnd(n, 31 + i) for i in range(B)])
+    z = rng.random((B, n))
+    x[z < 0.45] = 0.0
+    x[(z >= 0.45) & (z < 0.75)] = -0.0
+    for b in range(B):
+        for s0 in rng.integers(0, n - 4096, 8):
+            x[b, s0:s0 + int(rng.integers(64, 4096))] = -0.0 if s0 & 1 else 0.0
+    for lev in (1, 3, 6, 9):
+        yr = oracle.batch("wpt", True, w, x, lev)
+        assert_bits(T.wpt_forward(x, w, lev, ctx), yr, "%s wpt fwd l=%d" % (wname, lev))
+        # coefficients with signed-zero runs for the reverse
+        yz = yr.copy()
+        yz[z < 0.3] = -0.0
+        assert_bits(T.wpt_reverse(yz, w, lev, ctx), oracle.batch("wpt", False, w, yz, lev),
+                    "%s wpt rev l=%d" % (wname, lev))
+
+
 @pytest.mark.parametrize("B", [3, 64, 97])
 def test_wpt_batch_runs(ctx, B):
     """Batches whose rows the streamed kernels share out in runs of tiles
