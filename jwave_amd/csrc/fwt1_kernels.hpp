@@ -207,8 +207,11 @@ struct Rev1Geo {
 template <int L, int NT, int T, int K, bool FMA, int l, bool WT = false, bool CP = false,
           bool IP = false>
 struct Rev1Level {
+  // tl: the taps staged in LDS (stage_rev_taps; couples only): the array-head
+  // pairs' rotated order reads them at a runtime index
   __device__ __forceinline__ static void run(const RevTaps<L>& tp, double* lds, int t,
-                                             double* __restrict__ y, int sp = 0) {
+                                             double* __restrict__ y, int sp = 0,
+                                             const double* tl = nullptr) {
     using G = Rev1Geo<L, T, K>;
     JWV_STAMP(20 + l);
     constexpr int Q = G::Q;
@@ -328,8 +331,11 @@ struct Rev1Level {
       if (ml >= 0 && ml < np) {
         const int li = off + ml;
         double xe, xo;
-        rev_pair_rot<L, FMA>(tp, [=](int q) { return ab[li - q]; },
-                             [=](int q) { return db[li - q]; }, tid, xe, xo);
+        // rotation r = mg = tid at a runtime index: taps from LDS, not a
+        // Q x Q register select (~230 v_cndmask per level in wave 0 of every
+        // head tile: a quarter of config 3's row tiles)
+        rev_pair_rot_t<L, FMA>(tl, [=](int q) { return ab[li - q]; },
+                               [=](int q) { return db[li - q]; }, tid, xe, xo);
         put(NPUT - 1, ml, xe, xo, true);
       }
     }
@@ -341,7 +347,7 @@ struct Rev1Level {
     }
     if constexpr (l > 0) {
       lds_barrier();
-      Rev1Level<L, NT, T, K, FMA, l - 1, WT, CP, IP>::run(tp, lds, t, y, sp);
+      Rev1Level<L, NT, T, K, FMA, l - 1, WT, CP, IP>::run(tp, lds, t, y, sp, tl);
     }
   }
 };
@@ -361,6 +367,7 @@ __global__ __launch_bounds__(NT) void fwt_rev_tile1(const double* __restrict__ a
                                                     int64_t s_d, int hK, RevTaps<L> tp,
                                                     int sp, int lsw, int64_t ss) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ __attribute__((aligned(16))) double tl[2 * L];
   using G = Rev1Geo<L, T, K>;
   constexpr int MAXU = (G::len(1) + NT - 1) / NT;
   const int ntile = hK / T;
@@ -389,8 +396,9 @@ __global__ __launch_bounds__(NT) void fwt_rev_tile1(const double* __restrict__ a
                                return (int64_t)(i >> lsw) * ss + (i & sm);
                              });
   }
+  stage_rev_taps<L>(tp, tl);  // published by the barrier below
   dma_fence_barrier();
-  Rev1Level<L, NT, T, K, FMA, K - 1, false, true, IP>::run(tp, lds, t, dst + o * s_d, sp);
+  Rev1Level<L, NT, T, K, FMA, K - 1, false, true, IP>::run(tp, lds, t, dst + o * s_d, sp, tl);
 }
 
 }  // namespace jwv
