@@ -1053,10 +1053,11 @@ def test_fwt_denoise(ctx, wname, n, lev):
 
 def test_host_entry_staging_paths(ctx):
     """The host-pointer entries (Transform.forward(double[]) semantics) move
-    pageable arrays through the pinned staging ring in 8 MiB chunks and DMA
-    page-locked arrays (jwv_host_alloc) directly: every combination gives the
-    device entry's bits, for sizes that end mid-chunk, and the caller's
-    current device is left as it was."""
+    pageable arrays through the pinned staging ring (4 slots of 32 MiB; the
+    exposed end of each transfer ramps 2, 4, 8, 16 MiB, capi.cpp
+    stage_chunks) and DMA page-locked arrays (jwv_host_alloc) directly: every
+    combination gives the device entry's bits, for sizes that end mid-chunk
+    or wrap the ring, and the caller's current device is left as it was."""
     import ctypes
     import torch
     from jwave_amd import _lib as L
@@ -1064,7 +1065,7 @@ def test_host_entry_staging_paths(ctx):
     lib = L.lib()
     w = jw.by_class("Daubechies4")
     t = _TapsHolder.of(w)
-    for n, lev in ((1 << 22, 22), ((1 << 20) * 3, 0), (1 << 10, 10)):
+    for n, lev in ((1 << 22, 22), ((1 << 20) * 3, 0), (1 << 10, 10), (1 << 24, 24)):
         if lev == 0:  # 3 Mi doubles (not a power of two): AED path of one call
             x = rnd(n, 5)
             ref = T.aed_transform(torch.from_numpy(x).cuda(), w, "fwt", True, ctx).cpu().numpy()
