@@ -1053,9 +1053,8 @@ def test_fwt_denoise(ctx, wname, n, lev):
 
 def test_host_entry_staging_paths(ctx):
     """The host-pointer entries (Transform.forward(double[]) semantics) move
-    pageable arrays through the pinned staging ring (4 slots of 32 MiB; the
-    exposed end of each transfer ramps 2, 4, 8, 16 MiB, capi.cpp
-    stage_chunks) and DMA page-locked arrays (jwv_host_alloc) directly: every
+    pageable arrays through the pinned staging ring (4 slots of 32 MiB,
+    capi.cpp PinRing) and DMA page-locked arrays (jwv_host_alloc) directly: every
     combination gives the device entry's bits, for sizes that end mid-chunk
     or wrap the ring, and the caller's current device is left as it was."""
     import ctypes
