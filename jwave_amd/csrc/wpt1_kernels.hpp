@@ -32,6 +32,10 @@
 #ifndef JWV_WPT_HEADOVR
 #define JWV_WPT_HEADOVR 1
 #endif
+// JWV_WPT_FMA2: FMA mode's reverse couples as two FMAs per term (below)
+#ifndef JWV_WPT_FMA2
+#define JWV_WPT_FMA2 1
+#endif
 
 namespace jwv {
 
@@ -158,6 +162,32 @@ __device__ __forceinline__ void rev_couple_ilv(const RevTaps<L>& tp, const doubl
                                                double& e1, double& o1) {
   constexpr int QE = (L + 1) / 2, QO = L / 2;
   double se0 = 0.0, so0 = 0.0, se1 = 0.0, so1 = 0.0;
+  if constexpr (FMA && JWV_WPT_FMA2) {
+    // FMA mode: each term's two products go into the running sum as two
+    // fused multiply-adds (2 instructions per term instead of mul, fma, add;
+    // same terms, same term order, within FMA mode's 1e-12 contract)
+#pragma unroll
+    for (int q = QE - 1; q >= 0; --q) {
+      const double a0 = A[-q], d0 = D[-q], a1 = A[1 - q], d1 = D[1 - q];
+      se0 = __builtin_fma(a0, tp.lo_r[2 * q], se0);
+      se1 = __builtin_fma(a1, tp.lo_r[2 * q], se1);
+      if (q < QO) {
+        so0 = __builtin_fma(a0, tp.lo_r[2 * q + 1], so0);
+        so1 = __builtin_fma(a1, tp.lo_r[2 * q + 1], so1);
+      }
+      se0 = __builtin_fma(d0, tp.hi_r[2 * q], se0);
+      se1 = __builtin_fma(d1, tp.hi_r[2 * q], se1);
+      if (q < QO) {
+        so0 = __builtin_fma(d0, tp.hi_r[2 * q + 1], so0);
+        so1 = __builtin_fma(d1, tp.hi_r[2 * q + 1], so1);
+      }
+    }
+    e0 = se0;
+    o0 = so0;
+    e1 = se1;
+    o1 = so1;
+    return;
+  }
 #pragma unroll
   for (int q = QE - 1; q >= 0; --q) {
     const double a0 = A[-q], d0 = D[-q], a1 = A[1 - q], d1 = D[1 - q];
