@@ -32,6 +32,11 @@
 #ifndef JWV_WPT_HEADOVR
 #define JWV_WPT_HEADOVR 1
 #endif
+// JWV_WPT_HEADT: the reverse's array-head pairs in the rotated order with the
+// taps from LDS (rev_pair_rot_t) instead of rev_pair_head's two masked passes
+#ifndef JWV_WPT_HEADT
+#define JWV_WPT_HEADT 1
+#endif
 // JWV_WPT_FMA2: FMA mode's reverse couples as two FMAs per term (below)
 #ifndef JWV_WPT_FMA2
 #define JWV_WPT_FMA2 1
@@ -215,8 +220,10 @@ struct Wpt1RevLevel {
   // occur only in the first tiles: there, lanes tid < 2^(l-1)(Q-1) compute one
   // head pair each, and the couples skip storing them (one copy of the head
   // code per level instead of one per unrolled slot).
+  // tl: the taps staged in LDS (the head pairs' rotated order reads them at a
+  // runtime index, rev_pair_rot_t)
   __device__ __forceinline__ static void run(const RevTaps<L>& tp, double* lds, int t,
-                                             double* __restrict__ y) {
+                                             double* __restrict__ y, const double* tl) {
     using G = Wpt1RevGeo<L, T, K>;
     constexpr int Q = L / 2;
     constexpr int li_ = G::len(l), lo_ = G::len(l - 1);  // window strides in LDS
@@ -303,8 +310,13 @@ struct Wpt1RevLevel {
         const double* ab = lds + (2 * s) * li_;
         const double* db = ab + li_;
         const int li = off + ml;
+#if JWV_WPT_HEADT
+        rev_pair_rot_t<L, FMA>(tl, [=](int q) { return ab[li - q]; },
+                               [=](int q) { return db[li - q]; }, m, hxe, hxo);
+#else
         rev_pair_head<L, FMA>(
             tp, m, [=](int q) { return ab[li - q]; }, [=](int q) { return db[li - q]; }, hxe, hxo);
+#endif
         hs = s;
         hml = ml;
       }
@@ -338,7 +350,7 @@ struct Wpt1RevLevel {
       if (hs >= 0) *reinterpret_cast<double2*>(lds + hs * lo_ + 2 * hml) = make_double2(hxe, hxo);
 #endif
       lds_barrier();
-      Wpt1RevLevel<L, NT, T, K, FMA, l - 1, ILV>::run(tp, lds, t, y);
+      Wpt1RevLevel<L, NT, T, K, FMA, l - 1, ILV>::run(tp, lds, t, y, tl);
     }
   }
 };
@@ -350,6 +362,7 @@ __global__ __launch_bounds__(NT) void wpt_rev_tile1(const double* __restrict__ s
                                                     double* __restrict__ dst, AxisView dv, int h,
                                                     RevTaps<L> tp) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ __attribute__((aligned(16))) double tl[2 * L];
   using G = Wpt1RevGeo<L, T, K>;
   constexpr int LK = G::len(K);
   constexpr int NW = 1 << K;
@@ -368,8 +381,9 @@ __global__ __launch_bounds__(NT) void wpt_rev_tile1(const double* __restrict__ s
         const int w = e / LK, k = e - w * LK;
         return (int64_t)w * hp + ((BK + k) & pm);
       });
+  stage_rev_taps<L>(tp, tl);  // published by the barrier below
   dma_fence_barrier();
-  Wpt1RevLevel<L, NT, T, K, FMA, K, ILV>::run(tp, lds, t, dst + view_base(dv, o));
+  Wpt1RevLevel<L, NT, T, K, FMA, K, ILV>::run(tp, lds, t, dst + view_base(dv, o), tl);
 }
 
 }  // namespace jwv
