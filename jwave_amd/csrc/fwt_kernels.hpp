@@ -106,9 +106,6 @@ __device__ __forceinline__ void fwd_pair(const typename FB<L>::Fwd& tp, At at, d
 // again, so the same holds for every later level fed from it, and a level
 // that starts from +0.0 (ZS = true) restores Java's sign.  Used for the WPT
 // tiles' LDS-only levels; the level that writes HBM keeps ZS = true.
-#ifndef JWV_WPT_NZS
-#define JWV_WPT_NZS 1
-#endif
 // A couple's four sums (pairs at x and x + 2, analysis lo / hi) with the
 // products of G taps issued ahead of their adds: per group 4G independent
 // multiplies, then the 4G adds in the per-output order (j ascending), so no

@@ -22,25 +22,11 @@
 #pragma once
 #include "fwt1_kernels.hpp"
 
-// JWV_WPT_UDIV: slot -> (window, pair) by unsigned division (the signed
-// form costs a sign fix-up per slot).  JWV_WPT_HEADOVR: the reverse stores
-// every couple unpredicated; in the head tiles the array-head lanes rewrite
-// their pairs after one extra barrier.
-#ifndef JWV_WPT_UDIV
-#define JWV_WPT_UDIV 1
-#endif
-#ifndef JWV_WPT_HEADOVR
-#define JWV_WPT_HEADOVR 1
-#endif
-// JWV_WPT_HEADT: the reverse's array-head pairs in the rotated order with the
-// taps from LDS (rev_pair_rot_t) instead of rev_pair_head's two masked passes
-#ifndef JWV_WPT_HEADT
-#define JWV_WPT_HEADT 1
-#endif
-// JWV_WPT_FMA2: FMA mode's reverse couples as two FMAs per term (below)
-#ifndef JWV_WPT_FMA2
-#define JWV_WPT_FMA2 1
-#endif
+// Round 5 (profiles/r05o, r05p, r05u, r05v): unsigned slot
+// division, unpredicated reverse couple stores with the head pairs rewritten
+// after a head-tile barrier, head pairs from LDS-staged taps, LDS-only levels
+// without the +0.0 start (fwt_kernels.hpp ZS), FMA mode's reverse terms as two
+// FMAs.
 
 namespace jwv {
 
@@ -68,12 +54,8 @@ struct Wpt1FwdLevel {
     for (int r = 0; r < R; ++r) {
       const int q = tid + r * NT;
       if ((r + 1) * NT <= NC || q < NC) {
-#if JWV_WPT_UDIV
         const int s = (int)((unsigned)q / (unsigned)(mo / 2));       // sub-window
         const int i = (int)(2u * ((unsigned)q % (unsigned)(mo / 2)));  // first pair
-#else
-        const int s = q / (mo / 2), i = 2 * (q % (mo / 2));  // sub-window, first pair
-#endif
         wo[r] = (2 * s) * mo + i;
         const double* in = lds + s * mi + 2 * i;
         double x[L + 2];
@@ -85,7 +67,7 @@ struct Wpt1FwdLevel {
         }
         double a0, d0, a1, d1;
         if constexpr (JWV_WPT_FPIPE > 0 && !FMA) {
-          fwd_couple_pipe<L, FMA, (JWV_WPT_FPIPE < L ? JWV_WPT_FPIPE : L), !JWV_WPT_NZS || l == K>(
+          fwd_couple_pipe<L, FMA, (JWV_WPT_FPIPE < L ? JWV_WPT_FPIPE : L), l == K>(
               tp, x, a0, d0, a1, d1);
         } else {
           fwd_pair<L, FMA>(tp, [&](int j) { return x[j]; }, a0, d0);
@@ -167,7 +149,7 @@ __device__ __forceinline__ void rev_couple_ilv(const RevTaps<L>& tp, const doubl
                                                double& e1, double& o1) {
   constexpr int QE = (L + 1) / 2, QO = L / 2;
   double se0 = 0.0, so0 = 0.0, se1 = 0.0, so1 = 0.0;
-  if constexpr (FMA && JWV_WPT_FMA2) {
+  if constexpr (FMA) {
     // FMA mode: each term's two products go into the running sum as two
     // fused multiply-adds (2 instructions per term instead of mul, fma, add;
     // same terms, same term order, within FMA mode's 1e-12 contract)
@@ -246,12 +228,8 @@ struct Wpt1RevLevel {
     for (int r = 0; r < R; ++r) {
       const int k = tid + r * NT;
       if ((r + 1) * NT <= NC || k < NC) {
-#if JWV_WPT_UDIV
         const int s = (int)((unsigned)k / (unsigned)NCW);
         const int ml = (int)(2u * ((unsigned)k % (unsigned)NCW));
-#else
-        const int s = k / NCW, ml = 2 * (k % NCW);
-#endif
         const double* ab = lds + (2 * s) * li_;
         const double* db = ab + li_;
         const int st = off + ml - (Q - 1) - sh;  // even
@@ -271,7 +249,7 @@ struct Wpt1RevLevel {
         // pair ml: a[li - q] = av[(Q-1) + sh - q]; pair ml+1: one further
         double x0e, x0o, x1e, x1o;
         if constexpr (ILV && !FMA && JWV_WPT_RPIPE > 0 && (L / 2) % JWV_WPT_RPIPE == 0) {
-          rev_couple_pipe<L, JWV_WPT_RPIPE, !JWV_WPT_NZS || l == 1>(tp, av + (Q - 1) + sh, dv + (Q - 1) + sh, x0e, x0o,
+          rev_couple_pipe<L, JWV_WPT_RPIPE, l == 1>(tp, av + (Q - 1) + sh, dv + (Q - 1) + sh, x0e, x0o,
                                             x1e, x1o);
         } else if constexpr (ILV) {
           rev_couple_ilv<L, FMA>(tp, av + (Q - 1) + sh, dv + (Q - 1) + sh, x0e, x0o, x1e, x1o);
@@ -280,17 +258,10 @@ struct Wpt1RevLevel {
           rev_pair<L, FMA>(tp, av + Q + sh, dv + Q + sh, 1, x1e, x1o);
         }
         asm volatile("" : "+v"(x0e), "+v"(x0o), "+v"(x1e), "+v"(x1o) :: "memory");  // slot boundary
-#if JWV_WPT_HEADOVR
         // array-head pairs are stored like the others and overwritten by the
         // head lanes after one more barrier (head tiles only, below)
         const bool w0 = true;
         const bool w1 = (NPW % 2 == 0) || ml + 1 < NPW;
-#else
-        const int mg = pbase + ml;
-        const bool w0 = !(head_tile && mg >= 0 && mg < Q - 1);
-        const bool w1 = ((NPW % 2 == 0) || ml + 1 < NPW) &&
-                        !(head_tile && mg + 1 >= 0 && mg + 1 < Q - 1);
-#endif
         if constexpr (l == 1) {
           double* yo = y + (int64_t)t * T + 2 * ml;
           if (w0) *reinterpret_cast<double2*>(yo) = make_double2(x0e, x0o);
@@ -310,26 +281,17 @@ struct Wpt1RevLevel {
         const double* ab = lds + (2 * s) * li_;
         const double* db = ab + li_;
         const int li = off + ml;
-#if JWV_WPT_HEADT
         rev_pair_rot_t<L, FMA>(tl, [=](int q) { return ab[li - q]; },
                                [=](int q) { return db[li - q]; }, m, hxe, hxo);
-#else
-        rev_pair_head<L, FMA>(
-            tp, m, [=](int q) { return ab[li - q]; }, [=](int q) { return db[li - q]; }, hxe, hxo);
-#endif
         hs = s;
         hml = ml;
       }
     }
     if constexpr (l == 1) {
-#if JWV_WPT_HEADOVR
       if (head_tile) {
         __syncthreads();  // the couples' stores of the head pairs first (workgroup order)
         if (hs >= 0) *reinterpret_cast<double2*>(y + (int64_t)t * T + 2 * hml) = make_double2(hxe, hxo);
       }
-#else
-      if (hs >= 0) *reinterpret_cast<double2*>(y + (int64_t)t * T + 2 * hml) = make_double2(hxe, hxo);
-#endif
     } else {
       lds_barrier();
 #pragma unroll
@@ -341,14 +303,10 @@ struct Wpt1RevLevel {
           if (wo[r] & 2) *reinterpret_cast<double2*>(ob + 2) = make_double2(rx[r].z, rx[r].w);
         }
       }
-#if JWV_WPT_HEADOVR
       if (head_tile) {
         lds_barrier();
         if (hs >= 0) *reinterpret_cast<double2*>(lds + hs * lo_ + 2 * hml) = make_double2(hxe, hxo);
       }
-#else
-      if (hs >= 0) *reinterpret_cast<double2*>(lds + hs * lo_ + 2 * hml) = make_double2(hxe, hxo);
-#endif
       lds_barrier();
       Wpt1RevLevel<L, NT, T, K, FMA, l - 1, ILV>::run(tp, lds, t, y, tl);
     }
