@@ -34,6 +34,11 @@ namespace jwv {
 #else
 #define JWV_MOD_BAR() lds_barrier()
 #endif
+// JWV_MOD_NZS: the inverse's LDS-only levels start each sum at its first
+// product (ModInv1Level); A/B switch
+#ifndef JWV_MOD_NZS
+#define JWV_MOD_NZS 1
+#endif
 template <bool FMA>
 __device__ __forceinline__ double mod_mac(double acc, double a, double b) {
 #ifdef JWV_EXP_MOD_NOFP
@@ -401,9 +406,19 @@ struct ModInv1Level {
           aw1[l] = z.y;
         }
       }
+      // LDS-only levels (j > J0) start each sum at its first product (the
+      // signed-zero argument of fwt_kernels.hpp, ZS): one dependent add less
+      // per chain; the level that writes HBM starts from +0.0
+      constexpr bool kZ = j == J0 || !JWV_MOD_NZS;
       double sa0 = 0.0, sd0 = 0.0, sa1 = 0.0, sd1 = 0.0;
+      if constexpr (!kZ) {
+        sa0 = av0[0] * tp.g[0];
+        sd0 = aw0[0] * tp.h[0];
+        sa1 = av1[0] * tp.g[0];
+        sd1 = aw1[0] * tp.h[0];
+      }
 #pragma unroll
-      for (int l = 0; l < L; ++l) {
+      for (int l = kZ ? 0 : 1; l < L; ++l) {
         sa0 = mod_mac<FMA>(sa0, av0[l], tp.g[l]);
         sd0 = mod_mac<FMA>(sd0, aw0[l], tp.h[l]);
         sa1 = mod_mac<FMA>(sa1, av1[l], tp.g[l]);
@@ -464,12 +479,16 @@ struct ModInv1Level {
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         double s = 0.0;
+        constexpr bool kZ = j == J0 || !JWV_MOD_NZS;  // as in compute_p2
 #pragma unroll
         for (int l = 0; l < L; ++l) {
           // st = 1: output 2(s0+m)+q, tap l -> double 2m + q + l of the run;
           // st >= 2: slot m + l of the run, half q
           const double x = st == 1 ? v[2 * m + q + l] : v[2 * (m + l) + q];
-          s = mod_mac<FMA>(s, x, ISW ? tp.h[l] : tp.g[l]);
+          if (!kZ && l == 0)
+            s = x * (ISW ? tp.h[0] : tp.g[0]);
+          else
+            s = mod_mac<FMA>(s, x, ISW ? tp.h[l] : tp.g[l]);
         }
         acc[m][q] = s;
       }

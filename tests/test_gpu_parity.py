@@ -272,6 +272,27 @@ def test_wpt_signed_zeros(ctx, wname):
                     "%s wpt rev l=%d" % (wname, lev))
 
 
+@pytest.mark.parametrize("n,J", [(1 << 16, 8), (100003, 8), (50000, 5)])
+def test_modwt_signed_zeros(ctx, n, J):
+    """The MODWT inverse's LDS-only levels start each sum at its first
+    product (modwt1_kernels.hpp, JWV_MOD_NZS): inputs with +0.0 / -0.0 runs
+    (zero outputs of both product signs) must still give Java's bits at every
+    output, zero signs included, forward and inverse."""
+    w = jw.by_class("Daubechies4")
+    rng = np.random.default_rng(11)
+    x = rnd(n, 77)
+    z = rng.random(n)
+    x[z < 0.4] = 0.0
+    x[(z >= 0.4) & (z < 0.7)] = -0.0
+    for s0 in rng.integers(0, n - 3000, 6):
+        x[s0:s0 + int(rng.integers(300, 3000))] = -0.0 if s0 & 1 else 0.0
+    c_ref = oracle.modwt_forward(w, x, J)
+    assert_bits(T.modwt_forward(x, w, J, ctx), c_ref, "modwt fwd n=%d J=%d" % (n, J))
+    cz = c_ref.copy()
+    cz[:, rng.random(n) < 0.3] = -0.0
+    assert_bits(T.modwt_inverse(cz, w, ctx), oracle.modwt_inverse(w, cz), "modwt inv n=%d J=%d" % (n, J))
+
+
 @pytest.mark.parametrize("B", [3, 64, 97])
 def test_wpt_batch_runs(ctx, B):
     """Batches whose rows the streamed kernels share out in runs of tiles
