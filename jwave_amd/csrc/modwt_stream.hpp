@@ -139,13 +139,22 @@ struct ModFStream {
 #pragma unroll
       for (int l = 0; l < L; ++l) asm volatile("" : "+v"(x0[l]), "+v"(x1[l]));
     }
+    // V below the top level is LDS-only: its sums start at the first product
+    // (the signed-zero argument of fwt_kernels.hpp, ZS); W and V_J1 are
+    // outputs and start from +0.0
+    constexpr bool kZv = j == J1 || !JWV_MOD_NZS;
     double sw0 = 0.0, sv0 = 0.0, sw1 = 0.0, sv1 = 0.0;
 #pragma unroll
     for (int l = 0; l < L; ++l) {
       sw0 = mod_mac<FMA>(sw0, x0[l], tp.h[l]);
-      sv0 = mod_mac<FMA>(sv0, x0[l], tp.g[l]);
       sw1 = mod_mac<FMA>(sw1, x1[l], tp.h[l]);
-      sv1 = mod_mac<FMA>(sv1, x1[l], tp.g[l]);
+      if (!kZv && l == 0) {
+        sv0 = x0[0] * tp.g[0];
+        sv1 = x1[0] * tp.g[0];
+      } else {
+        sv0 = mod_mac<FMA>(sv0, x0[l], tp.g[l]);
+        sv1 = mod_mac<FMA>(sv1, x1[l], tp.g[l]);
+      }
     }
     pin2(sw0, sv0);
     pin2(sw1, sv1);
