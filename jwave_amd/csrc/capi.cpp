@@ -1665,7 +1665,8 @@ static void check_seg(int64_t rows, int64_t cols, int64_t seg) {
   if (rows < 0 || cols < 0) throw Fail{JWV_ERR_BAD_CALL, "negative dimension"};
   if (seg < 2 || (seg & (seg - 1)) || (cols && cols % seg) || seg > (int64_t(1) << 30))
     throw Fail{JWV_ERR_BAD_CALL, "seg must be a power of two >= 2 dividing cols"};
-  if (rows * cols > (int64_t(1) << 33)) throw Fail{JWV_ERR_BAD_CALL, "matrix too large"};
+  if (rows > (int64_t(1) << 30) || rows * cols > (int64_t(1) << 33))
+    throw Fail{JWV_ERR_BAD_CALL, "matrix too large"};
 }
 // [rows][cols] view <-> [cols/seg][rows][seg] copy: outer = chunk, len = row
 static Axis seg_pack_axis(const double* plain, double* segd, int64_t rows, int64_t cols,
@@ -1732,7 +1733,8 @@ static void check_2d(Kind k, bool fwd, int64_t rows, int64_t cols, int lvl_m, in
   // forward validates rows first (row pass), reverse the columns first
   if (fwd) { check_1d(k, true, cols, lvl_n); check_1d(k, true, rows, lvl_m); }
   else { check_1d(k, false, rows, lvl_m); check_1d(k, false, cols, lvl_n); }
-  if (rows * cols > (int64_t(1) << 33)) throw Fail{JWV_ERR_BAD_CALL, "matrix too large"};
+  if (rows > (int64_t(1) << 30) || rows * cols > (int64_t(1) << 33))
+    throw Fail{JWV_ERR_BAD_CALL, "matrix too large"};
 }
 
 #define JWV_2D(NAME, KIND, FWD)                                                                  \
