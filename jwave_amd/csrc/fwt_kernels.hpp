@@ -802,7 +802,6 @@ __global__ __launch_bounds__(NT) void fwt_rev_tile(const double* __restrict__ as
   const double* sa = asrc + view_base(as, o) + c0;
   const double* sc = coef + view_base(cv, o) + c0;
   double* y = dst + view_base(dv, o) + c0;
-  const int tid = threadIdx.x;
   double* abuf = lds;
   double* dall = lds + WA * C;
 
