@@ -93,10 +93,7 @@ hipError_t tile16_l(const Bank& b, const TileArgs& a, hipStream_t s, bool fwd) {
 }
 template <int L>
 hipError_t tile8_l(const Bank& b, const TileArgs& a, hipStream_t s, bool fwd) {
-#ifndef JWV_T16_FWD
-#define JWV_T16_FWD 1
-#endif
-  if (a.inner % 16 == 0 && (JWV_T16_FWD || !fwd)) {
+  if (a.inner % 16 == 0) {
     const int64_t hT = fwd ? (int64_t)a.h : ((int64_t)a.h << (a.K - 1));
     if (hT % (fwd ? kT16F : kT16R) == 0) return tile16_l<L>(b, a, s, fwd);
   }
