@@ -255,9 +255,6 @@ __global__ __launch_bounds__(NT, MINW) void fwt_rev_chain1(const double* __restr
 // and the whole-transform chains above when the data is MALL-warm.
 // ====================================================================
 
-#ifndef JWV_TAIL_XCD
-#define JWV_TAIL_XCD 1
-#endif
 // Forward tail: B units (tiles of TB level-input samples, KB levels; input =
 // the big pass's approximation, written by the previous launch) and, in the
 // block that completes the counter, the resident C levels.  Grid: hB / TB.
@@ -276,8 +273,8 @@ __global__ __launch_bounds__(NT) void fwt_fwd_tail1(const double* __restrict__ s
   // (round-robin dealing put every neighbour on another XCD: 2.6 x the input
   // from the fabric, r05g)
   const int tid = threadIdx.x, nU = gridDim.x;
-  const int u = JWV_TAIL_XCD && (nU & 7) == 0 ? (blockIdx.x & 7) * (nU >> 3) + (blockIdx.x >> 3)
-                                             : (int)blockIdx.x;
+  const int u = (nU & 7) == 0 ? (blockIdx.x & 7) * (nU >> 3) + (blockIdx.x >> 3)
+                              : (int)blockIdx.x;
   int* ctl = reinterpret_cast<int*>(lds + tail_ctl_off<L, TB, KB>(hB >> KB));
   {
     const int msk = hB - 1, base = u * TB;

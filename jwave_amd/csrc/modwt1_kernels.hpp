@@ -34,11 +34,6 @@ namespace jwv {
 #else
 #define JWV_MOD_BAR() lds_barrier()
 #endif
-// JWV_MOD_NZS: the inverse's LDS-only levels start each sum at its first
-// product (ModInv1Level); A/B switch
-#ifndef JWV_MOD_NZS
-#define JWV_MOD_NZS 1
-#endif
 template <bool FMA>
 __device__ __forceinline__ double mod_mac(double acc, double a, double b) {
 #ifdef JWV_EXP_MOD_NOFP
@@ -409,7 +404,7 @@ struct ModInv1Level {
       // LDS-only levels (j > J0) start each sum at its first product (the
       // signed-zero argument of fwt_kernels.hpp, ZS): one dependent add less
       // per chain; the level that writes HBM starts from +0.0
-      constexpr bool kZ = j == J0 || !JWV_MOD_NZS;
+      constexpr bool kZ = j == J0;
       double sa0 = 0.0, sd0 = 0.0, sa1 = 0.0, sd1 = 0.0;
       if constexpr (!kZ) {
         sa0 = av0[0] * tp.g[0];
@@ -479,7 +474,7 @@ struct ModInv1Level {
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         double s = 0.0;
-        constexpr bool kZ = j == J0 || !JWV_MOD_NZS;  // as in compute_p2
+        constexpr bool kZ = j == J0;  // as in compute_p2
 #pragma unroll
         for (int l = 0; l < L; ++l) {
           // st = 1: output 2(s0+m)+q, tap l -> double 2m + q + l of the run;

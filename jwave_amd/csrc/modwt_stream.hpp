@@ -142,7 +142,7 @@ struct ModFStream {
     // V below the top level is LDS-only: its sums start at the first product
     // (the signed-zero argument of fwt_kernels.hpp, ZS); W and V_J1 are
     // outputs and start from +0.0
-    constexpr bool kZv = j == J1 || !JWV_MOD_NZS;
+    constexpr bool kZv = j == J1;
     double sw0 = 0.0, sv0 = 0.0, sw1 = 0.0, sv1 = 0.0;
 #pragma unroll
     for (int l = 0; l < L; ++l) {
