@@ -34,14 +34,16 @@ typename MB<L>::Arg mtaps(const Bank& b) {
 
 template <typename K>
 hipError_t prep(K kernel, size_t lds) {
-  if (lds > 65536)
+  if (lds + sizeof(ModNf) > 65536)  // + the static repair words (modwt_nonfinite.hpp)
     return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   return hipSuccess;
 }
 
-unsigned level_grid(int64_t N) {
-  int64_t g = (N + 255) / 256;
+// blocks for a one-level kernel: chunks of modwt_level_chunk(j) outputs
+unsigned level_grid(int64_t N, int j) {
+  const int64_t B = modwt_level_chunk(j);
+  int64_t g = (N + B - 1) / B;
   return (unsigned)(g < 8192 ? (g > 0 ? g : 1) : 8192);
 }
 
@@ -69,7 +71,7 @@ hipError_t fwd_go(const Bank& b, bool tiled, const ModwtArgs& a, hipStream_t s) 
   }
   const auto tp = mtaps<L>(b);
   auto k = modwt_fwd_level<L, kFMA>;
-  JWV_LAUNCH(k, dim3(level_grid(a.N)), dim3(256), 0, s, a.src,
+  JWV_LAUNCH(k, dim3(level_grid(a.N, a.j0)), dim3(256), 0, s, a.src,
                      a.wout + (int64_t)(a.j0 - 1) * a.ldw, a.vout, a.N, a.j0, tp);
   return hipGetLastError();
 }
@@ -96,6 +98,10 @@ hipError_t inv_tile_cm_go(const Bank& b, const ModwtArgs& a, hipStream_t s) {
     auto k = modwt_inv_tile_cm<L, NTX, TX, SMAX, kFMA>;
     const int buf = ModCm::buf(TX, b.L, a.j0, a.j1);
     const size_t lds = (size_t)2 * buf * sizeof(double);
+    // The class padding grows with the stride: a deep level alone (Haar1 at
+    // j = 12: st = 2048, 6 doubles per class) needs more than a CU's LDS in
+    // this layout; the plain-layout tile needs 2 (T + R) doubles.
+    if (lds + sizeof(ModNf) > 160 * 1024) return inv_tile_go<L, NT, TI>(b, a, s);
     if (hipError_t e = prep(k, lds)) return e;
     const dim3 grid((unsigned)((a.N + TX - 1) / TX));
     JWV_LAUNCH(k, grid, dim3(NTX), lds, s, a.src, a.coef, a.ldw, a.vout, a.N, a.j0,
@@ -111,7 +117,7 @@ hipError_t inv_go(const Bank& b, bool tiled, const ModwtArgs& a, hipStream_t s) 
   }
   const auto tp = mtaps<L>(b);
   auto k = modwt_inv_level<L, kFMA>;
-  JWV_LAUNCH(k, dim3(level_grid(a.N)), dim3(256), 0, s, a.src,
+  JWV_LAUNCH(k, dim3(level_grid(a.N, a.j0)), dim3(256), 0, s, a.src,
                      a.coef + (int64_t)(a.j0 - 1) * a.ldw, a.vout, a.N, a.j0, tp);
   return hipGetLastError();
 }

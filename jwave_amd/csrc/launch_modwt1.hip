@@ -24,7 +24,7 @@ constexpr int kNT = 512, kTF = 4096, kTI = 2048;
 
 template <typename K>
 hipError_t prep(K kernel, size_t lds) {
-  if (lds > 65536)
+  if (lds + sizeof(ModNf) > 65536)  // + the static repair words (modwt_nonfinite.hpp)
     return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   return hipSuccess;

@@ -16,8 +16,13 @@
 //  * a slot fence every kFence slots bounds how many slots' reads the
 //    compiler hoists (registers), and the lane index is re-read per level
 //    (opaque_tid) so no level's addresses are kept live across the others.
+//
+// Non-finite input (modwt_nonfinite.hpp): each kernel runs its tile as a fast
+// pass that checks its last level's outputs and, in a block whose check
+// fired, again with SLOW = true (the Java zero-tap NaN repair).
 #pragma once
 #include "modwt_kernels.hpp"
+#include "modwt_nonfinite.hpp"
 
 namespace jwv {
 
@@ -131,7 +136,8 @@ struct ModFwd1Geo {
 // + e0 even, so every tap pair (e - l*st, e + 1 - l*st) is one 16-B LDS read
 // (st = 1: the 10-value run e-8 .. e+1) at a 16-B lane stride, and the W
 // pair (t0 - S + e even) is one 16-B store when the rows are 16-B aligned.
-template <int L, int NT, int T, int J0, int J1, bool FMA, int j, bool P2, int M = 1>
+template <int L, int NT, int T, int J0, int J1, bool FMA, int j, bool P2, int M = 1,
+          bool SLOW = false>
 struct ModFwd1Level {
   static constexpr int kPad = ModFwd1Geo<L, T, J0, J1>::kPad;
   // M = m + 100*jr: run form with m pairs per lane on levels j >= jr
@@ -139,19 +145,40 @@ struct ModFwd1Level {
   static constexpr bool kRun = kM > 1 && j >= kJR;
   __device__ __forceinline__ static void run_p2(const ModwtTaps<L>& tp, double* lds,
                                                 double* __restrict__ wout, int64_t ldw,
-                                                int64_t t0, int64_t N) {
+                                                int64_t t0, int64_t N, ModNf& nf) {
     using G = ModFwd1Geo<L, T, J0, J1>;
     constexpr int st = 1 << (j - 1);
     constexpr int e0 = G::e0(j), nout = G::nout(j);
     static_assert(((kPad + e0) & 1) == 0 && (nout & 1) == 0, "pairs must tile the outputs");
     constexpr int NP = nout / 2;
     constexpr int R = (NP + NT - 1) / NT;
+    // repair: window positions [e0 - C, S + T) at lds[kPad + q]
+    constexpr int C = (L - 1) * st;
+    int lo[2] = {1, 1}, hi[2] = {0, 0};
+    auto at = [&](int q) { return lds[kPad + q]; };
+    if constexpr (SLOW && j >= 2)
+      nf_window<1, NT>(nf, e0 - C, G::W, [&](int, int q) { return at(q); }, lo, hi);
     const int tid = opaque_tid();
     double* __restrict__ wrow = wout + (int64_t)(j - 1) * ldw + (t0 - G::S);
     // 16-B W stores: row base (j-1)*ldw + t0 - S + e is even for these e
     const bool w16 = (((uintptr_t)wrow + 8 * e0) & 15) == 0;
     // the whole tile inside the signal and 16-B rows: buffer stores
     const bool wfast = w16 && t0 + T <= N;
+    // repair mask (bit 2r + h: output e0 + 2k + h is Java's NaN), formed
+    // before the sums so the scans hold no sum registers
+    static_assert(2 * R <= 32, "repair mask bits");
+    uint32_t nm = 0;
+    if constexpr (SLOW && j >= 2)
+      if (lo[0] <= hi[0]) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int k = tid + r * NT;
+          const int e = e0 + 2 * ((r + 1) * NT <= NP ? k : (k < NP ? k : NP - 1));
+          if (nf_fwd_zero(at, e, st, C, lo[0], hi[0])) nm |= 1u << (2 * r);
+          if (nf_fwd_zero(at, e + 1, st, C, lo[0], hi[0])) nm |= 2u << (2 * r);
+        }
+        asm volatile("" : "+v"(nm)::"memory");
+      }
     double2 vv[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -190,6 +217,10 @@ struct ModFwd1Level {
         sw1 = mod_mac<FMA>(sw1, x1[l], tp.h[l]);
         sv1 = mod_mac<FMA>(sv1, x1[l], tp.g[l]);
       }
+      if constexpr (SLOW) {
+        if ((nm >> (2 * r)) & 1) sw0 = sv0 = mod_nan();
+        if ((nm >> (2 * r)) & 2) sw1 = sv1 = mod_nan();
+      }
       pin2(sw0, sv0);
       pin2(sw1, sv1);
       vv[r] = make_double2(sv0, sv1);
@@ -218,24 +249,24 @@ struct ModFwd1Level {
     }
     JWV_MOD_BAR();
     if constexpr (j < J1)
-      ModFwd1Level<L, NT, T, J0, J1, FMA, j + 1, P2, M>::run(tp, lds, wout, ldw, t0, N);
+      ModFwd1Level<L, NT, T, J0, J1, FMA, j + 1, P2, M, SLOW>::run(tp, lds, wout, ldw, t0, N, nf);
   }
   __device__ __forceinline__ static void run(const ModwtTaps<L>& tp, double* lds,
                                              double* __restrict__ wout, int64_t ldw, int64_t t0,
-                                             int64_t N) {
+                                             int64_t N, ModNf& nf) {
     static_assert(P2 && M == 1, "forward: the P2 form");
-    run_p2(tp, lds, wout, ldw, t0, N);
+    run_p2(tp, lds, wout, ldw, t0, N, nf);
   }
 };
 
-// src = V_{J0-1} (length N); W_j -> wout + (j-1)*ldw; V_{J1} -> vout.
-// Grid: ceil(N/T) blocks (XCD-aware order, xcd_tile).
-template <int L, int NT, int T, int J0, int J1, bool FMA, bool P2 = false, int M = 1>
-__global__ __launch_bounds__(NT) void modwt_fwd_tile1(const double* __restrict__ src,
-                                                      double* __restrict__ wout, int64_t ldw,
-                                                      double* __restrict__ vout, int64_t N,
-                                                      ModwtTaps<L> tp) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
+// One forward tile: window load, levels J0..J1, V_{J1} out.  The fast pass
+// (SLOW = false) ORs "a V_{J1} output is not finite" into bad.
+template <int L, int NT, int T, int J0, int J1, bool FMA, bool P2, int M, bool SLOW>
+__device__ __forceinline__ void modwt_fwd_tile1_body(const double* __restrict__ src,
+                                                     double* __restrict__ wout, int64_t ldw,
+                                                     double* __restrict__ vout, int64_t N,
+                                                     const ModwtTaps<L>& tp, double* lds,
+                                                     ModNf& nf, bool& bad) {
   using G = ModFwd1Geo<L, T, J0, J1>;
   constexpr int MAXP = (G::W + NT - 1) / NT;
   constexpr int pad = (P2 || M % 100 > 1) ? G::kPad : 0;
@@ -247,13 +278,36 @@ __global__ __launch_bounds__(NT) void modwt_fwd_tile1(const double* __restrict__
     load_window<1, NT, MAXP>(lds + pad, src, G::W, false, 0, 1,
                              [&](int e) { return wrap_mod(t0 - G::S + e, N); });
   JWV_MOD_BAR();
-  ModFwd1Level<L, NT, T, J0, J1, FMA, J0, P2, M>::run(tp, lds, wout, ldw, t0, N);
+  ModFwd1Level<L, NT, T, J0, J1, FMA, J0, P2, M, SLOW>::run(tp, lds, wout, ldw, t0, N, nf);
   const int tid = threadIdx.x;
 #pragma unroll
   for (int r = 0; r < (T + NT - 1) / NT; ++r) {
     const int p = tid + r * NT;
-    if (p < T && t0 + p < N) vout[t0 + p] = lds[pad + G::S + p];
+    if (p < T && t0 + p < N) {
+      const double v = lds[pad + G::S + p];
+      if constexpr (!SLOW) bad = bad || nonfinite(v);
+      vout[t0 + p] = v;
+    }
   }
+}
+
+// src = V_{J0-1} (length N); W_j -> wout + (j-1)*ldw; V_{J1} -> vout.
+// Grid: ceil(N/T) blocks (XCD-aware order, xcd_tile).
+template <int L, int NT, int T, int J0, int J1, bool FMA, bool P2 = false, int M = 1>
+__global__ __launch_bounds__(NT, mod_lds_waves(ModFwd1Geo<L, T, J0, J1>::lds_doubles(M) * 8, NT))
+void modwt_fwd_tile1(const double* __restrict__ src,
+                                                      double* __restrict__ wout, int64_t ldw,
+                                                      double* __restrict__ vout, int64_t N,
+                                                      ModwtTaps<L> tp) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ ModNf nf;
+  nf_init(nf);
+  bool bad = false;
+  modwt_fwd_tile1_body<L, NT, T, J0, J1, FMA, P2, M, false>(src, wout, ldw, vout, N, tp, lds, nf,
+                                                            bad);
+  if (nf_any(nf, bad))
+    modwt_fwd_tile1_body<L, NT, T, J0, J1, FMA, P2, M, true>(src, wout, ldw, vout, N, tp, lds, nf,
+                                                             bad);
 }
 
 // ---------------------------------------------------------------- inverse
@@ -291,7 +345,8 @@ struct ModInv1Geo {
 };
 
 
-template <int L, int NT, int T, int J0, int J1, bool FMA, int j, bool P2 = false, int M = 1>
+template <int L, int NT, int T, int J0, int J1, bool FMA, int j, bool P2 = false, int M = 1,
+          bool SLOW = false>
 struct ModInv1Level {
   using G = ModInv1Geo<L, T, J0, J1>;
   // M = m + 100*jr: run form with m pairs per lane on levels j >= jr
@@ -329,10 +384,31 @@ struct ModInv1Level {
       if (r * NT < Wn && ((r + 1) * NT <= Wn || q < Wn)) pw[r] = row[wrap_mod(t0 + q, N)];
     }
   }
+  using Next = ModInv1Level<L, NT, T, J0, J1, FMA, j - 1, P2, M, SLOW>;
+  // Repair state of a level: non-finite ranges of the V (0) and W (1) windows
+  struct Nf {
+    ModNf& f;
+    bool& bad;
+    int lo[2] = {1, 1}, hi[2] = {0, 0};
+  };
+  static constexpr int kC = (L - 1) * (1 << (j - 1));
+  // Java's NaN at output p (SLOW only; needs the level's windows intact)
+  __device__ __forceinline__ static bool nf_out(const Nf& nf, const double* vb, const double* wb,
+                                                int p) {
+    constexpr int st = 1 << (j - 1);
+    if constexpr (!SLOW || st == 1) {
+      return false;
+    } else {
+      return (nf.lo[0] <= nf.hi[0] &&
+              nf_inv_zero([&](int q) { return vb[q]; }, p, st, kC, nf.lo[0], nf.hi[0])) ||
+             (nf.lo[1] <= nf.hi[1] &&
+              nf_inv_zero([&](int q) { return wb[q]; }, p, st, kC, nf.lo[1], nf.hi[1]));
+    }
+  }
   __device__ __forceinline__ static void run(const ModwtTaps<L>& tp, double* vb, double* wb,
                                              double (&pw)[MAXP], const double* __restrict__ coef,
                                              int64_t ldw, double* __restrict__ dst, int64_t t0,
-                                             int64_t N, bool inside) {
+                                             int64_t N, bool inside, ModNf& f, bool& bad) {
     static_assert(P2, "inverse: the P2 or run form");
     constexpr int Wn = T + G::Rin(j);
     const int tid = opaque_tid();
@@ -342,12 +418,14 @@ struct ModInv1Level {
       if (r * NT < Wn && ((r + 1) * NT <= Wn || q < Wn)) wb[q] = pw[r];
     }
     JWV_MOD_BAR();
-    if constexpr (j > J0)
-      ModInv1Level<L, NT, T, J0, J1, FMA, j - 1, P2, M>::fetch(pw, coef, ldw, t0, N, inside);
+    if constexpr (j > J0) Next::fetch(pw, coef, ldw, t0, N, inside);
+    Nf nf{f, bad};
+    if constexpr (SLOW && j >= 2)
+      nf_window<2, NT>(f, 0, Wn, [&](int k, int q) { return k ? wb[q] : vb[q]; }, nf.lo, nf.hi);
     if constexpr (kRun)
-      compute_mr(tp, vb, wb, pw, coef, ldw, dst, t0, N, inside);
+      compute_mr(tp, vb, wb, pw, coef, ldw, dst, t0, N, inside, nf);
     else
-      compute_p2(tp, vb, wb, pw, coef, ldw, dst, t0, N, inside);
+      compute_p2(tp, vb, wb, pw, coef, ldw, dst, t0, N, inside, nf);
   }
   // P2: a lane computes the adjacent outputs (p, p+1), p even: every tap pair
   // (p + l*st, p + 1 + l*st) of V and of W is one 16-B LDS read (st = 1: the
@@ -357,12 +435,26 @@ struct ModInv1Level {
                                                     double (&pw)[MAXP],
                                                     const double* __restrict__ coef, int64_t ldw,
                                                     double* __restrict__ dst, int64_t t0,
-                                                    int64_t N, bool inside) {
+                                                    int64_t N, bool inside, Nf& nf) {
     constexpr int st = 1 << (j - 1);
     constexpr int nout = T + G::Rout(j);
     constexpr int NP = (nout + 1) / 2;
     constexpr int R = (NP + NT - 1) / NT;
     const int tid = opaque_tid();
+    // repair mask (bit 2r + h: output 2kc + h is Java's NaN), formed before
+    // the sums so the scans hold no sum registers
+    static_assert(2 * R <= 32, "repair mask bits");
+    uint32_t nm = 0;
+    if constexpr (SLOW) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int k = tid + r * NT;
+        const int kc = (r + 1) * NT <= NP ? k : (k < NP ? k : NP - 1);
+        if (nf_out(nf, vb, wb, 2 * kc)) nm |= 1u << (2 * r);
+        if (nf_out(nf, vb, wb, 2 * kc + 1)) nm |= 2u << (2 * r);
+      }
+      asm volatile("" : "+v"(nm)::"memory");
+    }
     double2 vv[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -422,6 +514,10 @@ struct ModInv1Level {
       pin2(sa0, sd0);
       pin2(sa1, sd1);
       vv[r] = make_double2(sa0 + sd0, sa1 + sd1);
+      if constexpr (SLOW) {
+        if ((nm >> (2 * r)) & 1) vv[r].x = mod_nan();
+        if ((nm >> (2 * r)) & 2) vv[r].y = mod_nan();
+      }
       if constexpr (JWV_MOD1_FENCE > 0)
         if ((r + 1) % JWV_MOD1_FENCE == 0)
           asm volatile("" : "+v"(vv[r].x), "+v"(vv[r].y) :: "memory");
@@ -434,6 +530,8 @@ struct ModInv1Level {
         const int k = tid + r * NT;
         const int p = 2 * k;
         if (r * NT * 2 < T && p < T) {
+          if constexpr (!SLOW)
+            nf.bad = nf.bad || nonfinite(vv[r].x) || (p + 1 < T && nonfinite(vv[r].y));
           if (dfast) {
             mod_store2(dst + t0, p, vv[r].x, vv[r].y);
           } else if (t0 + p + 1 < N && p + 1 < T) {
@@ -449,8 +547,7 @@ struct ModInv1Level {
         const int k = tid + r * NT;
         if ((r + 1) * NT <= NP || k < NP) *reinterpret_cast<double2*>(vb + 2 * k) = vv[r];
       }
-      ModInv1Level<L, NT, T, J0, J1, FMA, j - 1, P2, M>::run(tp, vb, wb, pw, coef, ldw, dst, t0, N,
-                                                          inside);
+      Next::run(tp, vb, wb, pw, coef, ldw, dst, t0, N, inside, nf.f, nf.bad);
     }
   }
   // Run form (ModRun): output pair slot s = s0 + m*h, m < M, reads tap slots
@@ -493,7 +590,7 @@ struct ModInv1Level {
                                                     double (&pw)[MAXP],
                                                     const double* __restrict__ coef, int64_t ldw,
                                                     double* __restrict__ dst, int64_t t0,
-                                                    int64_t N, bool inside) {
+                                                    int64_t N, bool inside, Nf& nf) {
     constexpr int st = 1 << (j - 1);
     constexpr int H = ModRun<L, kM>::template h<st>();
     constexpr int nout = G::nout(j);
@@ -503,6 +600,23 @@ struct ModInv1Level {
     constexpr int R = (NTASK + NT - 1) / NT;
     static_assert(G::run_reach(j, kM) <= G::run_buf(M), "run reads past the buffer");
     const int tid = opaque_tid();
+    // repair mask (bit 2(r kM + m) + h), formed before the sums
+    static_assert(2 * R * kM <= 32, "repair mask bits");
+    uint32_t nm = 0;
+    if constexpr (SLOW) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int t = tid + r * NT;
+        const int s0 = ModRun<L, kM>::template slot0<st>(t < NTASK ? t : NTASK - 1);
+#pragma unroll
+        for (int m = 0; m < kM; ++m) {
+          const int s = s0 + m * H;
+          if (nf_out(nf, vb, wb, 2 * s)) nm |= 1u << (2 * (r * kM + m));
+          if (nf_out(nf, vb, wb, 2 * s + 1)) nm |= 2u << (2 * (r * kM + m));
+        }
+      }
+      asm volatile("" : "+v"(nm)::"memory");
+    }
     double2 vv[R][kM];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -520,6 +634,10 @@ struct ModInv1Level {
         pin2(sa[m][0], sd[m][0]);
         pin2(sa[m][1], sd[m][1]);
         vv[r][m] = make_double2(sa[m][0] + sd[m][0], sa[m][1] + sd[m][1]);
+        if constexpr (SLOW) {
+          if ((nm >> (2 * (r * kM + m))) & 1) vv[r][m].x = mod_nan();
+          if ((nm >> (2 * (r * kM + m))) & 2) vv[r][m].y = mod_nan();
+        }
       }
       asm volatile("" ::: "memory");  // slot fence
     }
@@ -537,6 +655,8 @@ struct ModInv1Level {
         if constexpr (j == J0) {
           const int p = 2 * s;
           if (ok && p < T) {
+            if constexpr (!SLOW)
+              nf.bad = nf.bad || nonfinite(vv[r][m].x) || (p + 1 < T && nonfinite(vv[r][m].y));
             if (dfast) {
               mod_store2(dst + t0, p, vv[r][m].x, vv[r][m].y);
             } else if (t0 + p + 1 < N && p + 1 < T) {
@@ -550,21 +670,20 @@ struct ModInv1Level {
         }
       }
     }
-    if constexpr (j > J0)
-      ModInv1Level<L, NT, T, J0, J1, FMA, j - 1, P2, M>::run(tp, vb, wb, pw, coef, ldw, dst, t0, N,
-                                                          inside);
+    if constexpr (j > J0) Next::run(tp, vb, wb, pw, coef, ldw, dst, t0, N, inside, nf.f, nf.bad);
   }
 };
 
-// vsrc = V_{J1}; W_j at coef + (j-1)*ldw; output V_{J0-1} -> dst.
-template <int L, int NT, int T, int J0, int J1, bool FMA, bool P2 = false, int M = 1>
-__global__ __launch_bounds__(NT) void modwt_inv_tile1(const double* __restrict__ vsrc,
-                                                      const double* __restrict__ coef, int64_t ldw,
-                                                      double* __restrict__ dst, int64_t N,
-                                                      ModwtTaps<L> tp) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
+// One inverse tile (fast pass: SLOW = false, ORs "an output is not finite"
+// into bad).
+template <int L, int NT, int T, int J0, int J1, bool FMA, bool P2, int M, bool SLOW>
+__device__ __forceinline__ void modwt_inv_tile1_body(const double* __restrict__ vsrc,
+                                                     const double* __restrict__ coef, int64_t ldw,
+                                                     double* __restrict__ dst, int64_t N,
+                                                     const ModwtTaps<L>& tp, double* lds,
+                                                     ModNf& nf, bool& bad) {
   using G = ModInv1Geo<L, T, J0, J1>;
-  using Top = ModInv1Level<L, NT, T, J0, J1, FMA, J1, P2, M>;
+  using Top = ModInv1Level<L, NT, T, J0, J1, FMA, J1, P2, M, SLOW>;
   double* vb = lds;
   double* wb = lds + (M % 100 > 1 ? G::run_buf(M) : G::buf());
   const int64_t t0 = xcd_tile() * T;
@@ -576,7 +695,27 @@ __global__ __launch_bounds__(NT) void modwt_inv_tile1(const double* __restrict__
     load_window<1, NT, Top::MAXP>(vb, vsrc, G::Wmax, false, 0, 1,
                                   [&](int e) { return wrap_mod(t0 + e, N); });
   Top::fetch(pw, coef, ldw, t0, N, inside);
-  Top::run(tp, vb, wb, pw, coef, ldw, dst, t0, N, inside);
+  Top::run(tp, vb, wb, pw, coef, ldw, dst, t0, N, inside, nf, bad);
+}
+
+// vsrc = V_{J1}; W_j at coef + (j-1)*ldw; output V_{J0-1} -> dst.
+template <int L, int NT, int T, int J0, int J1, bool FMA, bool P2 = false, int M = 1>
+// (the fast pass alone needs up to 80 VGPRs from J1 = 3 on: 6 waves per SIMD)
+__global__ __launch_bounds__(NT, mod_lds_waves(ModInv1Geo<L, T, J0, J1>::lds_doubles(M) * 8, NT,
+                                               J1 - J0 >= 2 ? 6 : 8))
+void modwt_inv_tile1(const double* __restrict__ vsrc,
+                                                      const double* __restrict__ coef, int64_t ldw,
+                                                      double* __restrict__ dst, int64_t N,
+                                                      ModwtTaps<L> tp) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ ModNf nf;
+  nf_init(nf);
+  bool bad = false;
+  modwt_inv_tile1_body<L, NT, T, J0, J1, FMA, P2, M, false>(vsrc, coef, ldw, dst, N, tp, lds, nf,
+                                                            bad);
+  if (nf_any(nf, bad))
+    modwt_inv_tile1_body<L, NT, T, J0, J1, FMA, P2, M, true>(vsrc, coef, ldw, dst, N, tp, lds, nf,
+                                                             bad);
 }
 
 }  // namespace jwv

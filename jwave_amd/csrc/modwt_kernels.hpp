@@ -14,8 +14,13 @@
 // halo S = (L-1)(2^j1 - 2^(j0-1)) of V_{j0-1}; inverse a right halo of the
 // same size on V_j1 and on every W_j it reads.  Deep levels whose halo would
 // not fit run per level with a direct global gather (modwt_*_level).
+//
+// Non-finite input: every kernel here runs a fast pass that checks its last
+// level's outputs and, in a block whose check fired, a repair pass
+// (SLOW = true) with Java's zero-tap NaNs (modwt_nonfinite.hpp).
 #pragma once
 #include "jwv_device.hpp"
+#include "modwt_nonfinite.hpp"
 
 namespace jwv {
 
@@ -62,12 +67,12 @@ __device__ __forceinline__ int64_t xcd_tile() {
 
 // Forward, tiled.  src = V_{j0-1} (length N); W_j -> wout + (j-1)*ldw;
 // V_{j1} -> vout.  Grid: ceil(N/T) blocks.  LDS: (T + S) doubles.
-template <int L, int NT, int T, int SMAX, bool FMA>
-__global__ __launch_bounds__(NT) void modwt_fwd_tile(const double* __restrict__ src,
-                                                     double* __restrict__ wout, int64_t ldw,
-                                                     double* __restrict__ vout, int64_t N, int j0,
-                                                     int j1, typename MB<L>::Arg tp) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
+template <int L, int NT, int T, int SMAX, bool FMA, bool SLOW>
+__device__ __forceinline__ void modwt_fwd_tile_body(const double* __restrict__ src,
+                                                    double* __restrict__ wout, int64_t ldw,
+                                                    double* __restrict__ vout, int64_t N, int j0,
+                                                    int j1, const typename MB<L>::Arg& tp,
+                                                    double* lds, ModNf& nf, bool& bad) {
   constexpr int MAXP = (T + SMAX + NT - 1) / NT;
   const int nL = MB<L>::n(tp);
   const int S = (nL - 1) * ((1 << j1) - (1 << (j0 - 1)));
@@ -84,6 +89,11 @@ __global__ __launch_bounds__(NT) void modwt_fwd_tile(const double* __restrict__ 
     const int e0 = S - Sn;              // first output (window index)
     const int nout = T + Sn;
     double* wrow = wout + (int64_t)(j - 1) * ldw;
+    // repair: window positions [e0 - C, W) (C = Sj - Sn)
+    int lo[2] = {1, 1}, hi[2] = {0, 0};
+    if constexpr (SLOW)
+      if (st > 1)
+        nf_window<1, NT>(nf, e0 - (Sj - Sn), W, [&](int, int q) { return lds[q]; }, lo, hi);
     double vv[MAXP];
 #pragma unroll
     for (int r = 0; r < MAXP; ++r) {
@@ -97,6 +107,10 @@ __global__ __launch_bounds__(NT) void modwt_fwd_tile(const double* __restrict__ 
           sw = mac<FMA>(sw, v, tp.h[l]);
           sv = mac<FMA>(sv, v, tp.g[l]);
         }
+        if constexpr (SLOW)
+          if (lo[0] <= hi[0] &&
+              nf_fwd_zero([&](int q) { return lds[q]; }, e, st, Sj - Sn, lo[0], hi[0]))
+            sw = sv = mod_nan();
         vv[r] = sv;
         const int64_t g = t0 + (e - S);
         if (e >= S && g < N) wrow[g] = sw;
@@ -113,27 +127,80 @@ __global__ __launch_bounds__(NT) void modwt_fwd_tile(const double* __restrict__ 
   }
   for (int p = tid; p < T; p += NT) {
     const int64_t g = t0 + p;
-    if (g < N) vout[g] = lds[S + p];
+    if (g < N) {
+      const double v = lds[S + p];
+      if constexpr (!SLOW) bad = bad || nonfinite(v);
+      vout[g] = v;
+    }
   }
 }
 
-// Forward, one level, direct gather (deep levels).  Grid-stride over N.
-template <int L, bool FMA>
-__global__ __launch_bounds__(256) void modwt_fwd_level(const double* __restrict__ src,
-                                                       double* __restrict__ wrow,
-                                                       double* __restrict__ vout, int64_t N,
-                                                       int j, typename MB<L>::Arg tp) {
-  const int64_t st = (int64_t)1 << (j - 1);
-  for (int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x; n < N; n += (int64_t)gridDim.x * 256) {
+// (bounds: the fast pass's own occupancy, so the repair pass cannot lower it)
+template <int L, int NT, int T, int SMAX, bool FMA>
+__global__ __launch_bounds__(NT, L == 16 ? 5 : 6) void modwt_fwd_tile(const double* __restrict__ src,
+                                                     double* __restrict__ wout, int64_t ldw,
+                                                     double* __restrict__ vout, int64_t N, int j0,
+                                                     int j1, typename MB<L>::Arg tp) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ ModNf nf;
+  nf_init(nf);
+  bool bad = false;
+  modwt_fwd_tile_body<L, NT, T, SMAX, FMA, false>(src, wout, ldw, vout, N, j0, j1, tp, lds, nf,
+                                                  bad);
+  if (nf_any(nf, bad))
+    modwt_fwd_tile_body<L, NT, T, SMAX, FMA, true>(src, wout, ldw, vout, N, j0, j1, tp, lds, nf,
+                                                   bad);
+}
+
+// Forward, one level, direct gather (deep levels).  A block walks chunks of
+// B = max(256, st) consecutive outputs (grid-stride over chunks): the real taps
+// of a chunk's outputs then cover every position of their windows, so a
+// chunk whose outputs are all finite read only finite values, and the repair
+// runs per chunk (its window, C + B positions, scanned from global memory).
+__host__ __device__ inline int modwt_level_chunk(int j) {
+  return j - 1 > 8 ? 1 << (j - 1) : 256;
+}
+template <int L, bool FMA, bool SLOW>
+__device__ __forceinline__ void modwt_fwd_level_chunk(const double* __restrict__ src,
+                                                      double* __restrict__ wrow,
+                                                      double* __restrict__ vout, int64_t N, int j,
+                                                      const typename MB<L>::Arg& tp, int64_t c0,
+                                                      int B, ModNf& nf, bool& bad) {
+  const int st = 1 << (j - 1);
+  const int C = (MB<L>::n(tp) - 1) * st;
+  auto at = [&](int q) { return src[wrap_mod(c0 + q, N)]; };
+  int lo[2] = {1, 1}, hi[2] = {0, 0};
+  if constexpr (SLOW) nf_window<1, 256>(nf, -C, B, [&](int, int q) { return at(q); }, lo, hi);
+  for (int p = threadIdx.x; p < B && c0 + p < N; p += 256) {
+    const int64_t n = c0 + p;
     double sw = 0.0, sv = 0.0;
 #pragma unroll
     for (int l = 0; l < MB<L>::n(tp); ++l) {
-      const double v = src[wrap_mod(n - l * st, N)];
+      const double v = src[wrap_mod(n - (int64_t)l * st, N)];
       sw = mac<FMA>(sw, v, tp.h[l]);
       sv = mac<FMA>(sv, v, tp.g[l]);
     }
+    if constexpr (SLOW)
+      if (lo[0] <= hi[0] && nf_fwd_zero(at, p, st, C, lo[0], hi[0])) sw = sv = mod_nan();
+    if constexpr (!SLOW) bad = bad || nonfinite(sv);
     wrow[n] = sw;
     vout[n] = sv;
+  }
+}
+template <int L, bool FMA>
+__global__ __launch_bounds__(256, L == 16 ? 6 : 8) void modwt_fwd_level(const double* __restrict__ src,
+                                                       double* __restrict__ wrow,
+                                                       double* __restrict__ vout, int64_t N,
+                                                       int j, typename MB<L>::Arg tp) {
+  __shared__ ModNf nf;
+  nf_init(nf);
+  const int B = modwt_level_chunk(j);
+  int gen = 0;
+  for (int64_t c0 = (int64_t)blockIdx.x * B; c0 < N; c0 += (int64_t)gridDim.x * B) {
+    bool bad = false;
+    modwt_fwd_level_chunk<L, FMA, false>(src, wrow, vout, N, j, tp, c0, B, nf, bad);
+    if (j > 1 && nf_any(nf, bad, ++gen))
+      modwt_fwd_level_chunk<L, FMA, true>(src, wrow, vout, N, j, tp, c0, B, nf, bad);
   }
 }
 
@@ -141,12 +208,12 @@ __global__ __launch_bounds__(256) void modwt_fwd_level(const double* __restrict_
 // output V_{j0-1} -> dst.  LDS: 2 * (T + R) doubles.  The W window of the
 // next level is loaded into registers while the current level computes, so
 // each block pays one exposed HBM latency instead of one per level.
-template <int L, int NT, int T, int SMAX, bool FMA>
-__global__ __launch_bounds__(NT) void modwt_inv_tile(const double* __restrict__ vsrc,
-                                                     const double* __restrict__ coef, int64_t ldw,
-                                                     double* __restrict__ dst, int64_t N, int j0,
-                                                     int j1, typename MB<L>::Arg tp) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
+template <int L, int NT, int T, int SMAX, bool FMA, bool SLOW>
+__device__ __forceinline__ void modwt_inv_tile_body(const double* __restrict__ vsrc,
+                                                    const double* __restrict__ coef, int64_t ldw,
+                                                    double* __restrict__ dst, int64_t N, int j0,
+                                                    int j1, const typename MB<L>::Arg& tp,
+                                                    double* lds, ModNf& nf, bool& bad) {
   constexpr int MAXP = (T + SMAX + NT - 1) / NT;
   const int nL = MB<L>::n(tp);
   const int R = (nL - 1) * ((1 << j1) - (1 << (j0 - 1)));
@@ -179,6 +246,11 @@ __global__ __launch_bounds__(NT) void modwt_inv_tile(const double* __restrict__ 
     lds_barrier();
     if (j > j0) fetch_w(j - 1, T + Rn);  // next level's W, in flight during this level
     const int nout = T + Rn;
+    // repair: V and W window positions [0, T + Rj)
+    int lo[2] = {1, 1}, hi[2] = {0, 0};
+    if constexpr (SLOW)
+      if (st > 1)
+        nf_window<2, NT>(nf, 0, T + Rj, [&](int k, int q) { return k ? wb[q] : vb[q]; }, lo, hi);
     double vv[MAXP];
 #pragma unroll
     for (int r = 0; r < MAXP; ++r) {
@@ -191,6 +263,12 @@ __global__ __launch_bounds__(NT) void modwt_inv_tile(const double* __restrict__ 
           sd = mac<FMA>(sd, wb[p + l * st], tp.h[l]);
         }
         vv[r] = sa + sd;
+        if constexpr (SLOW)
+          if ((lo[0] <= hi[0] &&
+               nf_inv_zero([&](int q) { return vb[q]; }, p, st, Rj - Rn, lo[0], hi[0])) ||
+              (lo[1] <= hi[1] &&
+               nf_inv_zero([&](int q) { return wb[q]; }, p, st, Rj - Rn, lo[1], hi[1])))
+            vv[r] = mod_nan();
       }
     }
     lds_barrier();
@@ -198,7 +276,10 @@ __global__ __launch_bounds__(NT) void modwt_inv_tile(const double* __restrict__ 
 #pragma unroll
       for (int r = 0; r < MAXP; ++r) {
         const int p = tid + r * NT;
-        if (p < T && t0 + p < N) dst[t0 + p] = vv[r];
+        if (p < T && t0 + p < N) {
+          if constexpr (!SLOW) bad = bad || nonfinite(vv[r]);
+          dst[t0 + p] = vv[r];
+        }
       }
     } else {
 #pragma unroll
@@ -212,22 +293,71 @@ __global__ __launch_bounds__(NT) void modwt_inv_tile(const double* __restrict__ 
   }
 }
 
-// Inverse, one level, direct gather.
-template <int L, bool FMA>
-__global__ __launch_bounds__(256) void modwt_inv_level(const double* __restrict__ vsrc,
-                                                       const double* __restrict__ wrow,
-                                                       double* __restrict__ dst, int64_t N, int j,
-                                                       typename MB<L>::Arg tp) {
-  const int64_t st = (int64_t)1 << (j - 1);
-  for (int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x; n < N; n += (int64_t)gridDim.x * 256) {
+template <int L, int NT, int T, int SMAX, bool FMA>
+__global__ __launch_bounds__(NT, 4) void modwt_inv_tile(const double* __restrict__ vsrc,
+                                                     const double* __restrict__ coef, int64_t ldw,
+                                                     double* __restrict__ dst, int64_t N, int j0,
+                                                     int j1, typename MB<L>::Arg tp) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ ModNf nf;
+  nf_init(nf);
+  bool bad = false;
+  modwt_inv_tile_body<L, NT, T, SMAX, FMA, false>(vsrc, coef, ldw, dst, N, j0, j1, tp, lds, nf,
+                                                  bad);
+  if (nf_any(nf, bad))
+    modwt_inv_tile_body<L, NT, T, SMAX, FMA, true>(vsrc, coef, ldw, dst, N, j0, j1, tp, lds, nf,
+                                                   bad);
+}
+
+// Inverse, one level, direct gather, in chunks as modwt_fwd_level.
+template <int L, bool FMA, bool SLOW>
+__device__ __forceinline__ void modwt_inv_level_chunk(const double* __restrict__ vsrc,
+                                                      const double* __restrict__ wrow,
+                                                      double* __restrict__ dst, int64_t N, int j,
+                                                      const typename MB<L>::Arg& tp, int64_t c0,
+                                                      int B, ModNf& nf, bool& bad) {
+  const int st = 1 << (j - 1);
+  const int C = (MB<L>::n(tp) - 1) * st;
+  int lo[2] = {1, 1}, hi[2] = {0, 0};
+  if constexpr (SLOW)
+    nf_window<2, 256>(nf, 0, B + C, [&](int k, int q) {
+      const int64_t g = wrap_mod(c0 + q, N);
+      return k ? wrow[g] : vsrc[g];
+    }, lo, hi);
+  for (int p = threadIdx.x; p < B && c0 + p < N; p += 256) {
+    const int64_t n = c0 + p;
     double sa = 0.0, sd = 0.0;
 #pragma unroll
     for (int l = 0; l < MB<L>::n(tp); ++l) {
-      const int64_t k = wrap_mod(n + l * st, N);
+      const int64_t k = wrap_mod(n + (int64_t)l * st, N);
       sa = mac<FMA>(sa, vsrc[k], tp.g[l]);
       sd = mac<FMA>(sd, wrow[k], tp.h[l]);
     }
-    dst[n] = sa + sd;
+    double v = sa + sd;
+    if constexpr (SLOW)
+      if ((lo[0] <= hi[0] && nf_inv_zero([&](int q) { return vsrc[wrap_mod(c0 + q, N)]; }, p, st,
+                                         C, lo[0], hi[0])) ||
+          (lo[1] <= hi[1] && nf_inv_zero([&](int q) { return wrow[wrap_mod(c0 + q, N)]; }, p, st,
+                                         C, lo[1], hi[1])))
+        v = mod_nan();
+    if constexpr (!SLOW) bad = bad || nonfinite(v);
+    dst[n] = v;
+  }
+}
+template <int L, bool FMA>
+__global__ __launch_bounds__(256, L == 16 ? 6 : 8) void modwt_inv_level(const double* __restrict__ vsrc,
+                                                       const double* __restrict__ wrow,
+                                                       double* __restrict__ dst, int64_t N, int j,
+                                                       typename MB<L>::Arg tp) {
+  __shared__ ModNf nf;
+  nf_init(nf);
+  const int B = modwt_level_chunk(j);
+  int gen = 0;
+  for (int64_t c0 = (int64_t)blockIdx.x * B; c0 < N; c0 += (int64_t)gridDim.x * B) {
+    bool bad = false;
+    modwt_inv_level_chunk<L, FMA, false>(vsrc, wrow, dst, N, j, tp, c0, B, nf, bad);
+    if (j > 1 && nf_any(nf, bad, ++gen))
+      modwt_inv_level_chunk<L, FMA, true>(vsrc, wrow, dst, N, j, tp, c0, B, nf, bad);
   }
 }
 
@@ -278,13 +408,13 @@ struct ModCm {
   }
 };
 
-template <int L, int NT, int T, int SMAX, bool FMA>
-__global__ __launch_bounds__(NT) void modwt_inv_tile_cm(const double* __restrict__ vsrc,
-                                                        const double* __restrict__ coef,
-                                                        int64_t ldw, double* __restrict__ dst,
-                                                        int64_t N, int j0, int j1, int buf,
-                                                        ModwtTaps<L> tp) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
+template <int L, int NT, int T, int SMAX, bool FMA, bool SLOW>
+__device__ __forceinline__ void modwt_inv_tile_cm_body(const double* __restrict__ vsrc,
+                                                       const double* __restrict__ coef,
+                                                       int64_t ldw, double* __restrict__ dst,
+                                                       int64_t N, int j0, int j1, int buf,
+                                                       const ModwtTaps<L>& tp, double* lds,
+                                                       ModNf& nf, bool& bad) {
   constexpr int MAXP = (T + SMAX + NT - 1) / NT;
   constexpr int MAXI = (T + SMAX) / (2 * NT) + 2;  // item slots: nmb*st <= W/2 + st
   const int R = (L - 1) * ((1 << j1) - (1 << (j0 - 1)));
@@ -328,6 +458,18 @@ __global__ __launch_bounds__(NT) void modwt_inv_tile_cm(const double* __restrict
     if (j > j0) fetch(coef + (int64_t)(j - 2) * ldw, Wout);  // next level's W in flight
     const int nmb = ModCm::nmb(Wout, sh);
     const int nitems = nmb << sh;
+    // repair: V and W window positions [0, Win), class-major
+    const int msk = st - 1, C = (L - 1) * st;
+    auto atv = [&](int q) { return vb[(q & msk) * M + (q >> sh)]; };
+    auto atw = [&](int q) { return wb[(q & msk) * M + (q >> sh)]; };
+    int lo[2] = {1, 1}, hi[2] = {0, 0};
+    if constexpr (SLOW)
+      if (st > 1)
+        nf_window<2, NT>(nf, 0, Win, [&](int k, int q) { return k ? atw(q) : atv(q); }, lo, hi);
+    auto nan_at = [&](int p) {
+      return (lo[0] <= hi[0] && nf_inv_zero(atv, p, st, C, lo[0], hi[0])) ||
+             (lo[1] <= hi[1] && nf_inv_zero(atw, p, st, C, lo[1], hi[1]));
+    };
     double o0[MAXI], o1[MAXI];
 #pragma unroll
     for (int k = 0; k < MAXI; ++k) {
@@ -356,6 +498,11 @@ __global__ __launch_bounds__(NT) void modwt_inv_tile_cm(const double* __restrict
         }
         o0[k] = sa0 + sd0;
         o1[k] = sa1 + sd1;
+        if constexpr (SLOW) {
+          const int p = (u & (st - 1)) + ((2 * (u >> sh)) << sh);
+          if (nan_at(p)) o0[k] = mod_nan();
+          if (nan_at(p + st)) o1[k] = mod_nan();
+        }
       }
     }
     lds_barrier();
@@ -365,8 +512,14 @@ __global__ __launch_bounds__(NT) void modwt_inv_tile_cm(const double* __restrict
         const int u = tid + k * NT;
         if ((k + 1) * NT <= nitems || u < nitems) {
           const int p = (u & (st - 1)) + ((2 * (u >> sh)) << sh);
-          if (p < T && t0 + p < N) dst[t0 + p] = o0[k];
-          if (p + st < T && t0 + p + st < N) dst[t0 + p + st] = o1[k];
+          if (p < T && t0 + p < N) {
+            if constexpr (!SLOW) bad = bad || nonfinite(o0[k]);
+            dst[t0 + p] = o0[k];
+          }
+          if (p + st < T && t0 + p + st < N) {
+            if constexpr (!SLOW) bad = bad || nonfinite(o1[k]);
+            dst[t0 + p + st] = o1[k];
+          }
         }
       }
     } else {
@@ -387,6 +540,23 @@ __global__ __launch_bounds__(NT) void modwt_inv_tile_cm(const double* __restrict
       // (the barrier after the next level's W scatter orders these writes)
     }
   }
+}
+
+template <int L, int NT, int T, int SMAX, bool FMA>
+__global__ __launch_bounds__(NT) void modwt_inv_tile_cm(const double* __restrict__ vsrc,
+                                                        const double* __restrict__ coef,
+                                                        int64_t ldw, double* __restrict__ dst,
+                                                        int64_t N, int j0, int j1, int buf,
+                                                        ModwtTaps<L> tp) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ ModNf nf;
+  nf_init(nf);
+  bool bad = false;
+  modwt_inv_tile_cm_body<L, NT, T, SMAX, FMA, false>(vsrc, coef, ldw, dst, N, j0, j1, buf, tp,
+                                                     lds, nf, bad);
+  if (nf_any(nf, bad))
+    modwt_inv_tile_cm_body<L, NT, T, SMAX, FMA, true>(vsrc, coef, ldw, dst, N, j0, j1, buf, tp,
+                                                      lds, nf, bad);
 }
 
 }  // namespace jwv

@@ -26,8 +26,14 @@
 // 228-232 for modwt_inv_tile1) and for the WPT forward and reverse (carried
 // packet halos; every geometry 5-20% slower than wpt_fwd_tile1 /
 // wpt_rev_tile1).
+//
+// Non-finite input (modwt_nonfinite.hpp): the fast pass checks V_J1; a block
+// whose chunk saw a non-finite value runs the chunk again with SLOW = true,
+// which repairs the outputs Java's zero taps make NaN (prologue levels
+// included: their V values become the carries).
 #pragma once
 #include "modwt1_kernels.hpp"
+#include "modwt_nonfinite.hpp"
 
 namespace jwv {
 
@@ -163,16 +169,21 @@ struct ModFStream {
   }
 
   // ---- prologue: the carries left of the chunk (positions .. c0)
-  template <int j>
-  __device__ __forceinline__ static void pro_level(const ModwtTaps<L>& tp, double* lds) {
+  template <int j, bool SLOW>
+  __device__ __forceinline__ static void pro_level(const ModwtTaps<L>& tp, double* lds, ModNf& nf) {
     if constexpr (j < J1) {
       constexpr int nout = G::D(j), np = nout / 2, R = (np + NT - 1) / NT;
       static_assert(nout % 2 == 0, "even prologue extents");
-      const int tid = opaque_tid();
       // input V_{j-1} on [c0 - D(j-1), c0): output e reads index C(j) + e
       // (level 1: the x region, padded by one, so index 1 + C(1) + e = H(1) + e)
       const double* in = j == 1 ? lds + G::qx() : lds + G::q(j & 1 ? 1 : 0);
       constexpr int base = j == 1 ? G::H(1) : G::C(j);
+      // repair: window positions [-C(j), nout) at in[base + q]
+      int lo[2] = {1, 1}, hi[2] = {0, 0};
+      auto at = [&](int q) { return in[base + q]; };
+      if constexpr (SLOW && j >= 2)
+        nf_window<1, NT>(nf, -G::C(j), nout, [&](int, int q) { return at(q); }, lo, hi);
+      const int tid = opaque_tid();
       double* out = lds + G::q(j & 1 ? 0 : 1);
       double2 o[R];
 #pragma unroll
@@ -181,6 +192,11 @@ struct ModFStream {
         const int kc = (r + 1) * NT <= np ? k : (k < np ? k : np - 1);
         double2 w;
         pair<j>(tp, in, base + 2 * kc, w, o[r]);
+        if constexpr (SLOW && j >= 2)
+          if (lo[0] <= hi[0]) {
+            if (nf_fwd_zero(at, 2 * kc, 1 << (j - 1), G::C(j), lo[0], hi[0])) o[r].x = mod_nan();
+            if (nf_fwd_zero(at, 2 * kc + 1, 1 << (j - 1), G::C(j), lo[0], hi[0])) o[r].y = mod_nan();
+          }
       }
       lds_barrier();  // the input is dead (level 1: x overlaps the carries)
       constexpr int CS = G::C(j + 1);  // carry of V_j: its last C(j+1) values
@@ -195,21 +211,27 @@ struct ModFStream {
         }
       }
       lds_barrier();
-      pro_level<j + 1>(tp, lds);
+      pro_level<j + 1, SLOW>(tp, lds, nf);
     }
   }
 
   // ---- main loop, level j of tile p0
-  template <int j>
+  template <int j, bool SLOW>
   __device__ __forceinline__ static void level(const ModwtTaps<L>& tp, double* lds,
                                                const double* __restrict__ src,
                                                double* __restrict__ wout, int64_t ldw,
                                                double* __restrict__ vout, int64_t p0, int64_t pn,
-                                               int64_t N, double2 (&rx)[kQX]) {
+                                               int64_t N, double2 (&rx)[kQX], ModNf& nf,
+                                               bool& bad) {
     constexpr int R = T / 2 / NT;
     static_assert(R * 2 * NT == T, "T = 2 NT R");
-    const int tid = opaque_tid();
     const double* in = lds + G::buf(j & 1);
+    // repair: window positions [-C(j), T) at in[H(j) + q]
+    int lo[2] = {1, 1}, hi[2] = {0, 0};
+    auto at = [&](int q) { return in[G::H(j) + q]; };
+    if constexpr (SLOW && j >= 2)
+      nf_window<1, NT>(nf, -G::C(j), T, [&](int, int q) { return at(q); }, lo, hi);
+    const int tid = opaque_tid();
     // carries: the head of V_j's buffer (V_j tail of the tile to the left)
     // and the tail of this level's input V_{j-1} (j >= 2) for the tile to
     // the right, read before the sums, written after them
@@ -228,6 +250,21 @@ struct ModFStream {
     double2 w[R], v[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) pair<j>(tp, in, G::H(j) + 2 * (tid + r * NT), w[r], v[r]);
+    if constexpr (!SLOW && j == J1) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) bad = bad || nonfinite(v[r].x) || nonfinite(v[r].y);
+    }
+    if constexpr (SLOW && j >= 2)
+      if (lo[0] <= hi[0]) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            if (nf_fwd_zero(at, 2 * (tid + r * NT) + h, 1 << (j - 1), G::C(j), lo[0], hi[0])) {
+              (h ? w[r].y : w[r].x) = mod_nan();
+              (h ? v[r].y : v[r].x) = mod_nan();
+            }
+      }
     if constexpr (CS > 0) {
       double* cw = lds + G::carry0() + G::coff(j - 1);
 #pragma unroll
@@ -266,7 +303,39 @@ struct ModFStream {
       fetch<G::Wn(1)>(rx, src, pn - G::H(1), N);
     }
     lds_barrier();
-    if constexpr (j < J1) level<j + 1>(tp, lds, src, wout, ldw, vout, p0, pn, N, rx);
+    if constexpr (j < J1) level<j + 1, SLOW>(tp, lds, src, wout, ldw, vout, p0, pn, N, rx, nf, bad);
+  }
+
+  // the chunk of tiles [ta, tb): prologue, then the tiles left to right
+  template <bool SLOW>
+  __device__ __forceinline__ static void chunk(const ModwtTaps<L>& tp, double* lds,
+                                               const double* __restrict__ src,
+                                               double* __restrict__ wout, int64_t ldw,
+                                               double* __restrict__ vout, int64_t N, int64_t ta,
+                                               int64_t tb, ModNf& nf, bool& bad) {
+    double2 rx[kQX];
+    {
+      // prologue: x on [c0 - XP, c0) (XP even), then V_1 .. V_{J1-1} heads
+      const int64_t c0 = ta * T;
+      double2 px[kQP];
+      fetch<G::XP()>(px, src, c0 - G::XP(), N);
+      fetch<G::Wn(1)>(rx, src, c0 - G::H(1), N);  // the first tile's window
+      put<G::XP()>(lds + G::qx(), px);
+      lds_barrier();
+      pro_level<1, SLOW>(tp, lds, nf);
+    }
+    put<G::Wn(1)>(lds + G::buf(1), rx);
+    {
+      const int64_t pn = (ta + 1 < tb ? ta + 1 : ta) * T;
+      fetch<G::Wn(1)>(rx, src, pn - G::H(1), N);
+    }
+    lds_barrier();
+    for (int64_t t = ta; t < tb; ++t) {
+      // the window loaded during tile t is tile t+2's (past the chunk end: a
+      // tile of the chunk, never used)
+      const int64_t pn = (t + 2 < tb ? t + 2 : t) * T;
+      level<1, SLOW>(tp, lds, src, wout, ldw, vout, t * T, pn, N, rx, nf, bad);
+    }
   }
 };
 
@@ -279,34 +348,15 @@ __global__ __launch_bounds__(NT) void modwt_fwd_stream(const double* __restrict_
                                                        double* __restrict__ vout, int64_t N,
                                                        int64_t ntile, ModwtTaps<L> tp) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ ModNf nf;
   using S = ModFStream<L, NT, T, J1, FMA>;
-  using G = ModFStreamGeo<L, T, J1>;
   const int64_t b = blockIdx.x, nb = gridDim.x;
   const int64_t ta = b * ntile / nb, tb = (b + 1) * ntile / nb;
   if (ta >= tb) return;  // block-uniform (never with nb <= ntile)
-  double2 rx[S::kQX];
-  {
-    // prologue: x on [c0 - XP, c0) (XP even), then V_1 .. V_{J1-1} heads
-    const int64_t c0 = ta * T;
-    double2 px[S::kQP];
-    S::template fetch<G::XP()>(px, src, c0 - G::XP(), N);
-    S::template fetch<G::Wn(1)>(rx, src, c0 - G::H(1), N);  // the first tile's window
-    S::template put<G::XP()>(lds + G::qx(), px);
-    lds_barrier();
-    S::template pro_level<1>(tp, lds);
-  }
-  S::template put<G::Wn(1)>(lds + G::buf(1), rx);
-  {
-    const int64_t pn = (ta + 1 < tb ? ta + 1 : ta) * T;
-    S::template fetch<G::Wn(1)>(rx, src, pn - G::H(1), N);
-  }
-  lds_barrier();
-  for (int64_t t = ta; t < tb; ++t) {
-    // the window loaded during tile t is tile t+2's (past the chunk end: a
-    // tile of the chunk, never used)
-    const int64_t pn = (t + 2 < tb ? t + 2 : t) * T;
-    S::template level<1>(tp, lds, src, wout, ldw, vout, t * T, pn, N, rx);
-  }
+  nf_init(nf);
+  bool bad = false;
+  S::template chunk<false>(tp, lds, src, wout, ldw, vout, N, ta, tb, nf, bad);
+  if (nf_any(nf, bad)) S::template chunk<true>(tp, lds, src, wout, ldw, vout, N, ta, tb, nf, bad);
 }
 
 }  // namespace jwv

@@ -318,10 +318,22 @@ static void circular_convolve_adjoint(const double* s, int N, const double* f, i
   }
 }
 
+/* Count of non-finite samples at the circular positions a, a+1, .., a+len-1
+ * (0 <= a < N, len <= N) from the prefix counts P[0..N]. */
+static int64_t circ_count(const int64_t* P, int N, int64_t a, int64_t len) {
+  if (a + len <= N) return P[a + len] - P[a];
+  return (P[N] - P[a]) + P[a + len - N];
+}
+
 /* Same sums with the zero taps of the upsampled filter skipped: for finite
  * inputs adding x*0.0 (= +-0.0) to a sum that started at +0.0 never changes it,
- * so this is bit-identical to the loops above and ~2^(j-1) times faster.  Used
- * for large sizes; tests check the two agree bit for bit. */
+ * so the sum is bit-identical to the loops above and ~2^(j-1) times faster.
+ * A non-finite sample at a zero tap makes the loops above give NaN (x*0.0 is
+ * NaN for x = +-inf or NaN), so the outputs whose window (m = 0 .. M-1,
+ * M = (L-1)*stride + 1, wrapping mod N as often as it does) holds one at a
+ * zero tap are set to NaN: the window's non-finite count (prefix sums) minus
+ * the count at its L real taps.  Tests check the two forms agree bit for bit,
+ * NaN positions included. */
 static void circular_convolve_sparse(const double* s, int N, const double* f, int L, int stride,
                                      int adjoint, double* out) {
   for (int n = 0; n < N; n++) {
@@ -332,6 +344,26 @@ static void circular_convolve_sparse(const double* s, int N, const double* f, in
     }
     out[n] = sum;
   }
+  if (stride == 1 || N == 0) return;
+  int64_t* P = (int64_t*)malloc(sizeof(int64_t) * ((size_t)N + 1));
+  P[0] = 0;
+  for (int i = 0; i < N; i++) P[i + 1] = P[i] + !isfinite(s[i]);
+  const int64_t bad = P[N];
+  if (bad > 0) {
+    const int64_t M = (int64_t)(L - 1) * stride + 1, full = M / N, rem = M % N;
+    for (int n = 0; n < N; n++) {
+      /* forward: positions n, n-1, .., n-M+1; adjoint: n, n+1, .., n+M-1 */
+      const int64_t a = adjoint ? n : floor_mod((int64_t)n - rem + 1, N);
+      const int64_t cnt = full * bad + (rem ? circ_count(P, N, a, rem) : 0);
+      int64_t real = 0;
+      for (int l = 0; l < L; l++) {
+        int64_t m = (int64_t)l * stride;
+        real += !isfinite(s[floor_mod(adjoint ? (int64_t)n + m : (int64_t)n - m, N)]);
+      }
+      if (cnt > real) out[n] = NAN;
+    }
+  }
+  free(P);
 }
 
 /* MODWTTransform.forwardMODWT — MODWTTransform.java:256-306.  out is

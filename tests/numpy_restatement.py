@@ -128,3 +128,53 @@ def modwt_inverse(w, c):
             d = d + c[j - 1][(n + l * s) % N] * h[l]
         v = a + d
     return v
+
+
+def _upsample(f, s):
+    """MODWTTransform.upsample (MODWTTransform.java:618-630): s - 1 zeros between taps."""
+    u = np.zeros((len(f) - 1) * s + 1)
+    u[::s] = f
+    return u
+
+
+def modwt_forward_dense(w, x, J):
+    """forwardMODWT with circularConvolve as written (MODWTTransform.java:677-690):
+    every tap of the upsampled filter, zeros included, m ascending.  Differs from
+    modwt_forward only on non-finite input (x * 0.0 is NaN for x = +-inf / NaN)."""
+    g, h = modwt_filters(w)
+    N = len(x)
+    v = np.array(x, dtype=np.float64)
+    n = np.arange(N)
+    out = []
+    for j in range(1, J + 1):
+        gu, hu = _upsample(g, 1 << (j - 1)), _upsample(h, 1 << (j - 1))
+        W = np.zeros(N)
+        V = np.zeros(N)
+        with np.errstate(invalid="ignore", over="ignore"):
+            for m in range(len(gu)):
+                src = v[(n - m) % N]
+                W = W + src * hu[m]
+                V = V + src * gu[m]
+        out.append(W)
+        v = V
+    out.append(v)
+    return np.stack(out)
+
+
+def modwt_inverse_dense(w, c):
+    """inverseMODWT with circularConvolveAdjoint as written (MODWTTransform.java:703-716)."""
+    g, h = modwt_filters(w)
+    J = c.shape[0] - 1
+    N = c.shape[1]
+    n = np.arange(N)
+    v = np.array(c[J])
+    for j in range(J, 0, -1):
+        gu, hu = _upsample(g, 1 << (j - 1)), _upsample(h, 1 << (j - 1))
+        a = np.zeros(N)
+        d = np.zeros(N)
+        with np.errstate(invalid="ignore", over="ignore"):
+            for m in range(len(gu)):
+                a = a + v[(n + m) % N] * gu[m]
+                d = d + c[j - 1][(n + m) % N] * hu[m]
+            v = a + d
+    return v

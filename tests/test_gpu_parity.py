@@ -622,6 +622,160 @@ def test_modwt_direct_vs_sparse_oracle():
     assert_exact(oracle.modwt_forward(w, x, 5, sparse=True), oracle.modwt_forward(w, x, 5, sparse=False))
 
 
+# ------------------------------------------------------------------ non-finite input
+NONFINITE = (np.inf, -np.inf, np.nan)
+
+
+def assert_nan_bits(got, ref, what=""):
+    """NaN at the same positions and every other value bit for bit (NaN
+    payloads are not compared: Java's NaN is the JVM's, the GPU's is its
+    canonical quiet NaN)."""
+    got = np.ascontiguousarray(np.asarray(got), dtype=np.float64).ravel()
+    ref = np.ascontiguousarray(ref, dtype=np.float64).ravel()
+    gn, rn = np.isnan(got), np.isnan(ref)
+    bad = np.flatnonzero(gn != rn)
+    assert bad.size == 0, "%s: NaN positions differ at %d places, first %d (got %r ref %r)" % (
+        what, bad.size, bad[0], got[bad[0]], ref[bad[0]])
+    gb, rb = got[~rn].view(np.int64), ref[~rn].view(np.int64)
+    bad = np.flatnonzero(gb != rb)
+    assert bad.size == 0, "%s: %d values differ in their bits, first at %d" % (what, bad.size, bad[0])
+
+
+def assert_nan_close(got, ref, what=""):
+    """FMA mode: the same NaN and +-inf positions, the rest within the gate."""
+    got = np.asarray(got, dtype=np.float64).ravel()
+    ref = np.asarray(ref, dtype=np.float64).ravel()
+    assert np.array_equal(np.isnan(got), np.isnan(ref)), what + ": NaN positions"
+    assert np.array_equal(np.isposinf(got), np.isposinf(ref)), what + ": +inf positions"
+    assert np.array_equal(np.isneginf(got), np.isneginf(ref)), what + ": -inf positions"
+    m = np.isfinite(ref)
+    assert_close(got[m], ref[m], what)
+
+
+def _edges(n, tiles=(1024, 2048, 4096, 8192)):
+    """Positions at and around the tile edges of every MODWT kernel geometry,
+    the wrap (0, n-1) and the middle."""
+    p = {0, 1, n - 1, n - 2, n // 2}
+    for t in tiles:
+        for k in range(1, min(n // t, 3) + 1):
+            p.update((k * t - 1, k * t))
+    return sorted(q for q in p if 0 <= q < n)
+
+
+def _inject(x, pos, rng):
+    x = x.copy()
+    pos = np.asarray(pos)
+    x[..., pos] = rng.choice(NONFINITE, size=x[..., pos].shape)
+    return x
+
+
+@pytest.mark.parametrize("wname", ["Haar1", "Daubechies4", "Daubechies8", "Symlet8", "CDF53",
+                                   "Daubechies20"])
+def test_modwt_nonfinite(ctx, wname):
+    """MODWTTransform.java:677-716 multiplies every zero tap of the upsampled
+    filter: +-inf / NaN at a zero tap of an output's window gives NaN there,
+    which the real-tap sums alone would miss (modwt_nonfinite.hpp).  One to
+    three non-finite values at tile edges, across the wrap and in the middle,
+    for every kernel form (streamed forward, compile-time and runtime tiles,
+    deep one-level kernels), forward and inverse, against the oracle (its
+    sparse path follows the same rule; test_oracle pins it to the DIRECT
+    loops)."""
+    w = jw.by_class(wname)
+    rng = np.random.default_rng(17)
+    for n in (8, 100, 1000, 4097, 5636, 12345, 20000):
+        full = n.bit_length() - 1
+        for J in sorted({1, 2, min(5, full), min(8, full), min(13, full) if n >= 20000 else 1}):
+            edges = _edges(n)
+            for trial in range(3):
+                pos = rng.choice(edges, size=int(rng.integers(1, 4)), replace=False)
+                x = _inject(rnd(n, n + trial), pos, rng)
+                cr = oracle.modwt_forward(w, x, J)
+                assert_nan_bits(T.modwt_forward(x, w, J, ctx), cr, "%s fwd n=%d J=%d" % (wname, n, J))
+                c = oracle.modwt_forward(w, rnd(n, 3 + trial), J)
+                rows = rng.integers(0, J + 1, len(pos))
+                c[rows, pos] = rng.choice(NONFINITE, size=len(pos))
+                assert_nan_bits(T.modwt_inverse(c, w, ctx), oracle.modwt_inverse(w, c),
+                                "%s inv n=%d J=%d" % (wname, n, J))
+
+
+@pytest.mark.parametrize("J", [2, 8, 13])
+def test_modwt_nonfinite_direct(ctx, J):
+    """The GPU against the oracle's as-written DIRECT loops (sparse=False, every
+    zero tap multiplied) at J = 2, 8 and 13: +inf, -inf and NaN at a tile
+    edge, across the wrap and in the middle, forward and inverse."""
+    w = jw.by_class("Daubechies4")
+    n = 20000
+    x = rnd(n, 91)
+    x[[0, 1023, 1024, n // 2]] = [np.nan, np.inf, -np.inf, np.nan]
+    x[n - 1] = np.inf
+    cd = oracle.modwt_forward(w, x, J, sparse=False)
+    assert_nan_bits(T.modwt_forward(x, w, J, ctx), cd, "fwd J=%d" % J)
+    c = oracle.modwt_forward(w, rnd(n, 92), J)
+    c[0, 2047] = np.inf
+    c[J, 2048] = -np.inf
+    c[J // 2, n - 1] = np.nan
+    assert_nan_bits(T.modwt_inverse(c, w, ctx), oracle.modwt_inverse(w, c, sparse=False), "inv J=%d" % J)
+
+
+def test_modwt_nonfinite_config5(ctx, ctx_fma):
+    """Config 5 (Daubechies4, J = 8, N = 10^7): non-finite samples at streamed
+    tile and chunk edges, across the wrap and inside, forward and inverse;
+    EXACT bit for bit (NaN positions) against the oracle, FMA with the same
+    NaN / inf positions."""
+    w = jw.by_class("Daubechies4")
+    n = 10_000_000
+    rng = np.random.default_rng(23)
+    pos = [0, 1, 1023, 1024, 2047, 2048, 13 * 1024, 4_999_999, 5_000_000, 7_777_777, n - 2, n - 1]
+    x = _inject(rnd(n, 42), pos, rng)
+    cr = oracle.modwt_forward(w, x, 8)
+    assert_nan_bits(T.modwt_forward(x, w, 8, ctx), cr, "modwt 1e7 fwd")
+    assert_nan_close(T.modwt_forward(x, w, 8, ctx_fma), cr, "modwt 1e7 fwd fma")
+    c = oracle.modwt_forward(w, rnd(n, 43), 8)
+    c[rng.integers(0, 9, len(pos)), pos] = rng.choice(NONFINITE, size=len(pos))
+    xr = oracle.modwt_inverse(w, c)
+    assert_nan_bits(T.modwt_inverse(c, w, ctx), xr, "modwt 1e7 inv")
+    assert_nan_close(T.modwt_inverse(c, w, ctx_fma), xr, "modwt 1e7 inv fma")
+
+
+def test_modwt_nonfinite_overflow_and_all_nan(ctx):
+    """Finite input whose level-1 sum overflows (inf meets level 2's zero
+    taps), and an all-NaN signal (every block repairs)."""
+    w = jw.by_class("Daubechies4")
+    g, _ = oracle.modwt_filters(w)
+    n = 100_000
+    x = rnd(n, 5)
+    x[50_000 - np.arange(len(g))] = np.sign(g) * 1.7e308
+    assert np.isfinite(x).all()
+    cr = oracle.modwt_forward(w, x, 8)
+    assert np.isnan(cr).any()
+    assert_nan_bits(T.modwt_forward(x, w, 8, ctx), cr, "overflow fwd")
+    x = np.full(n, np.nan)
+    assert np.isnan(np.asarray(T.modwt_forward(x, w, 8, ctx))).all()
+    assert np.isnan(np.asarray(T.modwt_inverse(np.full((9, n), np.nan), w, ctx))).all()
+
+
+@pytest.mark.parametrize("wname", ["Daubechies4", "Symlet8", "Haar1", "CDF53"])
+def test_fwt_wpt_nonfinite(ctx, wname):
+    """FWT / WPT have no zero taps (Wavelet.java:236-303), so the kernels'
+    sums already meet +-inf / NaN in Java's order: same NaN and inf positions
+    and bits as the oracle, forward and reverse, resident and tiled sizes."""
+    w = jw.by_class(wname)
+    rng = np.random.default_rng(29)
+    for n in (1024, 1 << 16):
+        pos = _edges(n)
+        x = _inject(rnd(n, 9), rng.choice(pos, size=3, replace=False), rng)
+        for lev in (1, 4, n.bit_length() - 1):
+            assert_nan_bits(T.fwt_forward(x, w, lev, ctx), oracle.fwt_forward(w, x, lev),
+                            "%s fwt fwd n=%d l=%d" % (wname, n, lev))
+            assert_nan_bits(T.fwt_reverse(x, w, lev, ctx), oracle.fwt_reverse(w, x, lev),
+                            "%s fwt rev n=%d l=%d" % (wname, n, lev))
+            if lev <= 9:
+                assert_nan_bits(T.wpt_forward(x, w, lev, ctx), oracle.wpt_forward(w, x, lev),
+                                "%s wpt fwd n=%d l=%d" % (wname, n, lev))
+                assert_nan_bits(T.wpt_reverse(x, w, lev, ctx), oracle.wpt_reverse(w, x, lev),
+                                "%s wpt rev n=%d l=%d" % (wname, n, lev))
+
+
 # ------------------------------------------------------------------ KATs on GPU
 def test_haar_kat_gpu(ctx):
     """CrossValidationTest.testHaarTransformWithReference (CrossValidationTest.java:187-211)."""

@@ -219,6 +219,67 @@ def test_oracle_modwt_equals_numpy(cls):
     assert np.array_equal(np.stack(oracle.modwt_filters(w)), np.stack(npr.modwt_filters(w)))
 
 
+NONFINITE = (np.inf, -np.inf, np.nan)
+
+
+def assert_nan_bits(got, ref, what=""):
+    """NaN at the same positions and every other value bit for bit (NaN
+    payloads and signs are not compared: the JVM's NaN is not specified)."""
+    got = np.ascontiguousarray(got, dtype=np.float64).ravel()
+    ref = np.ascontiguousarray(ref, dtype=np.float64).ravel()
+    gn, rn = np.isnan(got), np.isnan(ref)
+    bad = np.flatnonzero(gn != rn)
+    assert bad.size == 0, "%s: NaN positions differ at %d places, first %d (got %r ref %r)" % (
+        what, bad.size, bad[0], got[bad[0]], ref[bad[0]])
+    gb, rb = got[~rn].view(np.int64), ref[~rn].view(np.int64)
+    bad = np.flatnonzero(gb != rb)
+    assert bad.size == 0, "%s: %d values differ in their bits" % (what, bad.size)
+
+
+@pytest.mark.parametrize("cls", ["Haar1", "Daubechies4", "Symlet8", "CDF53"])
+def test_oracle_modwt_nonfinite_sparse_equals_direct(cls):
+    """MODWTTransform.java:677-716 multiplies every zero tap of the upsampled
+    filter too, so a +-inf / NaN sample at a zero tap of an output's window
+    makes that output NaN.  The oracle's sparse path (real taps plus the
+    zero-tap NaN rule) must equal the as-written DIRECT loops bit for bit,
+    NaN positions included, and so must the numpy restatement of the DIRECT
+    loops; windows longer than N (wrapping several times) included."""
+    w = jw.by_class(cls)
+    rng = np.random.default_rng(3)
+    more_nan = 0
+    for n, J in ((8, 3), (37, 2), (37, 5), (100, 5), (300, 6), (1000, 8)):
+        for trial in range(4):
+            x = oracle.java_random_doubles(11 + trial, n)
+            k = int(rng.integers(1, 4))
+            x[rng.choice(n, size=k, replace=False)] = rng.choice(NONFINITE, size=k)
+            cd = oracle.modwt_forward(w, x, J, sparse=False)
+            assert_nan_bits(oracle.modwt_forward(w, x, J, sparse=True), cd, "fwd n=%d J=%d" % (n, J))
+            assert_nan_bits(npr.modwt_forward_dense(w, x, J), cd, "numpy fwd n=%d J=%d" % (n, J))
+            with np.errstate(invalid="ignore", over="ignore"):
+                more_nan += int(np.isnan(cd).sum() > np.isnan(npr.modwt_forward(w, x, J)).sum())
+            c = oracle.modwt_forward(w, oracle.java_random_doubles(5, n), J)
+            c[rng.integers(0, J + 1, k), rng.integers(0, n, k)] = rng.choice(NONFINITE, size=k)
+            xd = oracle.modwt_inverse(w, c, sparse=False)
+            assert_nan_bits(oracle.modwt_inverse(w, c, sparse=True), xd, "inv n=%d J=%d" % (n, J))
+            assert_nan_bits(npr.modwt_inverse_dense(w, c), xd, "numpy inv n=%d J=%d" % (n, J))
+    # the rule is not vacuous: the zero taps add NaNs the real-tap sums lack
+    assert more_nan > 0
+
+
+def test_oracle_modwt_overflow_sparse_equals_direct():
+    """Finite input whose sums overflow: inf from one level meets the next
+    level's zero taps (NaN in Java), exactly as an inf input would."""
+    w = jw.by_class("Daubechies4")
+    g, _ = oracle.modwt_filters(w)
+    x = oracle.java_random_doubles(3, 500)
+    x[100 - np.arange(len(g))] = np.sign(g) * 1.7e308  # V_1[100] = sum |g| * 1.7e308
+    assert np.abs(g).sum() * 1.7e308 > np.finfo(np.float64).max
+    cd = oracle.modwt_forward(w, x, 6, sparse=False)
+    assert np.isinf(cd[0:6]).any() and np.isnan(cd).any()
+    assert np.isfinite(x).all()
+    assert_nan_bits(oracle.modwt_forward(w, x, 6, sparse=True), cd, "overflow fwd")
+
+
 def test_oracle_2d_3d_equal_loops():
     """2-D/3-D oracle == explicit per-line loops of the 1-D oracle (BasicTransform.java:361-659)."""
     w = jw.by_class("Daubechies4")
