@@ -76,7 +76,9 @@ int jwv_ctx_destroy(jwv_ctx* ctx);
 const char* jwv_last_error(const jwv_ctx* ctx);
 /* Launch on a caller-owned hipStream_t (NULL = the legacy default stream);
  * jwv_ctx_reset_stream returns to the context's own non-blocking stream
- * (the default after jwv_ctx_create). */
+ * (the default after jwv_ctx_create).  Switching streams makes the new stream
+ * wait (an event, no host sync) for the work the context queued on the old
+ * one, so its workspace and fused-tail counter stay ordered. */
 int jwv_ctx_set_stream(jwv_ctx* ctx, void* hip_stream);
 int jwv_ctx_reset_stream(jwv_ctx* ctx);
 void* jwv_ctx_get_stream(const jwv_ctx* ctx);
@@ -123,10 +125,10 @@ int jwv_ctx_profile_read(jwv_ctx* ctx, jwv_kernel_stat* out, int max_out, int* n
 int jwv_ctx_profile_select(jwv_ctx* ctx, const char* kind);
 /* Release cached device workspace and the pinned staging ring.
  * A context owns its workspace and its fused-tail arrival counters: it runs
- * one transform at a time (calls on one context are
- * serialised), and work it queued on one stream must have completed before
- * the context is pointed at another stream (jwv_ctx_set_stream) whose work is
- * not ordered after it.  Footprint: device workspace as large as the largest
+ * one transform at a time (calls on one context are serialised), and a stream
+ * switch orders the new stream after the old one (jwv_ctx_set_stream).  Work
+ * other code queues on the old stream after the switch is not ordered before
+ * the context's next launch.  Footprint: device workspace as large as the largest
  * transform's intermediates (one matrix for 2-D / 3-D), plus, once a host
  * entry staged pageable memory, 4 x 32 MiB of pinned host memory; the host
  * copy threads are one process-wide pool. */

@@ -43,24 +43,36 @@ public final class HipNative {
   // multi-context per process (its calls are serialised; each runs one host
   // thread per device).
   private static long MCTX = -1L;
+  // A bad jwave.hip.devices (unparsable, or a device the runtime rejects) is
+  // remembered and rethrown on every batch call: the setting never falls back
+  // to one device silently after its first failure.
+  private static String MCTX_ERROR = null;
 
   static synchronized long mctx( ) {
+    if( MCTX_ERROR != null )
+      throw new IllegalStateException( MCTX_ERROR );
     if( MCTX >= 0 )
       return MCTX;
-    MCTX = 0L;
     String p = System.getProperty( "jwave.hip.devices" );
     if( p == null || p.trim( ).isEmpty( ) )
-      return MCTX;
+      return MCTX = 0L;
     String[ ] parts = p.trim( ).split( "\\s*,\\s*" );
     if( parts.length < 2 )
-      return MCTX;
+      return MCTX = 0L;
     int[ ] dev = new int[ parts.length ];
-    for( int i = 0; i < dev.length; i++ )
-      dev[ i ] = Integer.parseInt( parts[ i ] );
+    try {
+      for( int i = 0; i < dev.length; i++ )
+        dev[ i ] = Integer.parseInt( parts[ i ] );
+    } catch( NumberFormatException e ) {
+      MCTX_ERROR = "jwave.hip.devices: not a device list: " + p;
+      throw new IllegalStateException( MCTX_ERROR );
+    }
     long[ ] h = new long[ 1 ];
     int rc = mctxCreate( dev, h );
-    if( rc != OK )
-      throw new IllegalStateException( mctxLastError( 0L ) );
+    if( rc != OK ) {
+      MCTX_ERROR = "jwave.hip.devices=" + p + ": " + mctxLastError( 0L );
+      throw new IllegalStateException( MCTX_ERROR );
+    }
     MCTX = h[ 0 ];
     return MCTX;
   }

@@ -167,6 +167,7 @@ struct jwv_ctx {
   unsigned epoch = 0;  // reverse flag value of the last call (never 0)
   unsigned poll_limit = 1u << 22;  // bound of every in-kernel wait (chained reverse)
   bool waited = false;  // a launch with an in-kernel wait is queued, timeout word unchecked
+  hipEvent_t switch_ev = nullptr;  // orders a stream switch after the old stream's work
   int plan = -1;       // JWV_PLAN_* bits; -1 = env defaults
   // profiling: hipEvent pairs around every kernel launch on the launch stream
   bool prof = false;
@@ -417,17 +418,24 @@ unsigned* sync_words(jwv_ctx* c) {
 }
 unsigned* tail_counter(jwv_ctx* c) { return sync_words(c) + 2 * ChainGeo::kWords + 16; }
 // Error path: a failed call may have left a tail launch part-way, so the
-// counter's value is unknown.  Drain the stream and zero the counter and its
-// base together (best effort: if the device is gone the context is too).
-void tail_resync(jwv_ctx* c) {
-  if (!c->sync || !c->tail_dirty) return;
-  c->tail_dirty = false;
+// counter's value is unknown.  Drain the stream, zero the counter on it and
+// drain again, then zero the base.  tail_dirty is cleared only when all of
+// that succeeded; otherwise the next call of the context retries first
+// (guarded), so no launch ever runs against a stale base.
+bool tail_resync(jwv_ctx* c) {
+  if (!c->sync || !c->tail_dirty) return true;
   int prev = -1;
   if (hipGetDevice(&prev) != hipSuccess || (prev != c->device && hipSetDevice(c->device) != hipSuccess))
-    return;
-  (void)hipStreamSynchronize(c->stream);
-  if (hipMemset(tail_counter(c), 0, sizeof(unsigned)) == hipSuccess) c->tail_base = 0;
+    return false;
+  const bool ok = hipStreamSynchronize(c->stream) == hipSuccess &&
+                  hipMemsetAsync(tail_counter(c), 0, sizeof(unsigned), c->stream) == hipSuccess &&
+                  hipStreamSynchronize(c->stream) == hipSuccess;
+  if (ok) {
+    c->tail_base = 0;
+    c->tail_dirty = false;
+  }
   if (prev != c->device) (void)hipSetDevice(prev);
+  return ok;
 }
 
 int plan_of(jwv_ctx* c) { return c->plan >= 0 ? c->plan : ChainGeo::default_plan(); }
@@ -915,6 +923,8 @@ int guarded(jwv_ctx* c, F&& f) {
   try {
     c->err.clear();
     DeviceScope ds(c->device);
+    if (c->tail_dirty && !tail_resync(c))  // an earlier failure's reset did not complete
+      throw Fail{JWV_ERR_DEVICE, "context unusable: resetting the fused-tail counter failed"};
     f();
     c->tail_dirty = false;
     return JWV_OK;
@@ -1474,6 +1484,7 @@ int jwv_ctx_destroy(jwv_ctx* c) {
   if (c->sync) hipFree(c->sync);
   for (auto& r : c->recs) { hipEventDestroy(r.e0); hipEventDestroy(r.e1); }
   for (auto e : c->ev_pool) hipEventDestroy(e);
+  if (c->switch_ev) hipEventDestroy(c->switch_ev);
   for (int i = 0; i < kPinSlots; ++i) {
     if (c->pin.p[i]) hipHostFree(c->pin.p[i]);
     if (c->pin.ev[i]) hipEventDestroy(c->pin.ev[i]);
@@ -1486,18 +1497,28 @@ int jwv_ctx_destroy(jwv_ctx* c) {
 
 const char* jwv_last_error(const jwv_ctx* c) { return c ? c->err.c_str() : g_tls_error.c_str(); }
 
+// Work a context queued on its old stream (workspace reads and writes, the
+// fused tail's arrival counter) must finish before anything it queues on the
+// new one: the new stream waits on an event recorded on the old one, so
+// alternating streams from one context is ordered without a host sync.
+static int switch_stream(jwv_ctx* c, hipStream_t s) {
+  if (s == c->stream) return JWV_OK;
+  return guarded(c, [&] {
+    if (!c->switch_ev) HIPCHK(hipEventCreateWithFlags(&c->switch_ev, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(c->switch_ev, c->stream));
+    HIPCHK(hipStreamWaitEvent(s, c->switch_ev, 0));
+    c->stream = s;
+  });
+}
+
 int jwv_ctx_set_stream(jwv_ctx* c, void* s) {
   if (!c) return set_err(nullptr, JWV_ERR_BAD_CALL, "jwv_ctx is NULL");
-  std::lock_guard<std::mutex> lk(c->mu);
-  c->stream = (hipStream_t)s;  // NULL = the legacy default stream
-  return JWV_OK;
+  return switch_stream(c, (hipStream_t)s);  // NULL = the legacy default stream
 }
 
 int jwv_ctx_reset_stream(jwv_ctx* c) {
   if (!c) return set_err(nullptr, JWV_ERR_BAD_CALL, "jwv_ctx is NULL");
-  std::lock_guard<std::mutex> lk(c->mu);
-  c->stream = c->own;
-  return JWV_OK;
+  return switch_stream(c, c->own);
 }
 
 void* jwv_ctx_get_stream(const jwv_ctx* c) { return c ? (void*)c->stream : nullptr; }

@@ -111,6 +111,13 @@ def _check_2d(rows, cols, W):
                          "(%d x %d over %d ranks)" % (rows, cols, W))
 
 
+def _segmentable(cw):
+    """The segmented row passes (jwv_fwt_rows_seg_*) take chunks of a power of
+    two >= 2 columns (capi.cpp check_seg); one-column chunks (cols == W) take
+    the plain pass and one packing copy."""
+    return cw >= 2 and (cw & (cw - 1)) == 0
+
+
 def _rows_to_send(x_rows, w, level, W, backend, kind):
     """Row pass whose result is the all-to-all send buffer [W][rw][cw] (chunk
     j -> rank j).  A backend with rows_to_chunks (HipBackend, FWT) writes
@@ -118,7 +125,7 @@ def _rows_to_send(x_rows, w, level, W, backend, kind):
     with one copy."""
     rw, C = x_rows.shape
     cw = C // W
-    if kind == "fwt" and hasattr(backend, "rows_to_chunks"):
+    if kind == "fwt" and _segmentable(cw) and hasattr(backend, "rows_to_chunks"):
         return backend.rows_to_chunks(x_rows, w, level, cw)
     a = backend.rows(x_rows, w, level, True, kind)
     return a.reshape(rw, W, cw).permute(1, 0, 2).contiguous()
@@ -128,7 +135,7 @@ def _recv_to_rows(recv, w, level, backend, kind):
     """Reverse row pass reading the all-to-all receive buffer [W][rw][cw]
     (chunk j = my rows of rank j's columns) in place where the backend can."""
     W, rw, cw = recv.shape
-    if kind == "fwt" and hasattr(backend, "chunks_to_rows"):
+    if kind == "fwt" and _segmentable(cw) and hasattr(backend, "chunks_to_rows"):
         return backend.chunks_to_rows(recv, w, level)
     return backend.rows(recv.permute(1, 0, 2).reshape(rw, W * cw), w, level, False, kind)
 

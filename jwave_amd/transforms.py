@@ -80,6 +80,10 @@ class Context:
     def set_stream(self, stream_handle):
         self._check(self._lib.jwv_ctx_set_stream(self.handle, stream_handle))
 
+    def reset_stream(self):
+        """Back to the context's own stream (ordered after the current one)."""
+        self._check(self._lib.jwv_ctx_reset_stream(self.handle))
+
     def synchronize(self):
         self._check(self._lib.jwv_ctx_synchronize(self.handle))
 
@@ -362,8 +366,9 @@ def fwt_rows_to_chunks(x, wavelet, level, seg, ctx=None):
         raise JWaveError("fwt_rows_to_chunks takes a [rows][cols] float64 device tensor")
     rows, cols = (int(v) for v in x.shape)
     seg = int(seg)
-    if seg < 1 or cols % seg:
-        raise JWaveError("fwt_rows_to_chunks: seg must divide cols (%d, %d)" % (seg, cols))
+    if seg < 2 or (seg & (seg - 1)) or cols % seg:
+        raise JWaveError("fwt_rows_to_chunks: seg must be a power of two >= 2 dividing cols "
+                         "(%d, %d)" % (seg, cols))
     return _run(None, "jwv_fwt_rows_seg_fwd_f64_dev", ctx, x, (cols // seg, rows, seg),
                 (rows, cols, int(level), seg, _TapsHolder.of(wavelet)))
 

@@ -52,7 +52,14 @@ class ChunkedOracleBackend(OracleBackend):
     rows, laid out as jwv_fwt_rows_seg_* lay them out: [cols/seg][rows][seg]),
     so the gloo runs exercise the exchange without pack / unpack copies."""
 
+    @staticmethod
+    def _check_seg(seg):
+        # the native entries' rule (capi.cpp check_seg)
+        if seg < 2 or seg & (seg - 1):
+            raise ValueError("seg must be a power of two >= 2 dividing cols")
+
     def rows_to_chunks(self, x, w, level, seg):
+        self._check_seg(seg)
         y = oracle.batch("fwt", True, w, x.numpy(), level)
         rows, cols = y.shape
         return torch.from_numpy(np.ascontiguousarray(
@@ -60,6 +67,7 @@ class ChunkedOracleBackend(OracleBackend):
 
     def chunks_to_rows(self, y, w, level):
         nch, rows, seg = y.shape
+        self._check_seg(seg)
         plain = np.ascontiguousarray(y.numpy().transpose(1, 0, 2).reshape(rows, nch * seg))
         return torch.from_numpy(oracle.batch("fwt", False, w, plain, level))
 
@@ -111,7 +119,9 @@ def main():
     for kind, wname, rows, cols, lm, ln in (
             ("fwt", "Daubechies8", 64, 128, 6, 7), ("fwt", "Haar1", 32, 16, 2, 3),
             ("fwt", "Daubechies4", 128, 64, 5, 0), ("fwt", "Daubechies4", 8, 4096, 3, 12),
-            ("wpt", "Symlet8", 64, 64, 4, 5)):
+            ("wpt", "Symlet8", 64, 64, 4, 5),
+            # cols == W: one-column chunks take the plain pass + packing copy
+            ("fwt", "Haar1", 4, 2, 2, 1)):
         if rows % W or cols % W:
             continue
         w = jw.by_class(wname)

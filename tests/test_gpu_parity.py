@@ -834,6 +834,42 @@ def test_device_tensors_and_stream(ctx):
     assert_exact(xr.cpu().numpy(), oracle.fwt_reverse(w, yr, 16), "dev rev")
 
 
+def test_alternating_streams_one_context(ctx):
+    """Two torch streams, one context, no host sync between the calls: each
+    stream switch (jwv_ctx_set_stream) makes the new stream wait for the old
+    one's work, so the fused forward tail's arrival counter and the shared
+    workspace stay ordered (config-2 plan at 2^20 and 2^22)."""
+    import torch
+    w = jw.by_class("Daubechies4")
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    try:
+        _alternate(ctx, w, s1, s2)
+    finally:
+        ctx.reset_stream()  # before s1 / s2 go away
+        torch.cuda.synchronize()
+
+
+def _alternate(ctx, w, s1, s2):
+    import torch
+    for n in (1 << 20, 1 << 22):
+        lev = n.bit_length() - 1
+        xs = [rnd(n, 50 + i) for i in range(6)]
+        xt = [torch.from_numpy(x).cuda() for x in xs]
+        torch.cuda.synchronize()
+        ys, rs = [], []
+        for i, x in enumerate(xt):
+            with torch.cuda.stream(s1 if i % 2 == 0 else s2):
+                y = T.fwt_forward(x, w, lev, ctx)
+                ys.append(y)
+                rs.append(T.fwt_reverse(y, w, lev, ctx))
+        torch.cuda.synchronize()
+        for i, x in enumerate(xs):
+            yr = oracle.fwt_forward(w, x, lev)
+            assert_exact(ys[i].cpu().numpy(), yr, "stream-alternating fwd n=%d #%d" % (n, i))
+            assert_exact(rs[i].cpu().numpy(), oracle.fwt_reverse(w, yr, lev),
+                         "stream-alternating rev n=%d #%d" % (n, i))
+
+
 def test_facade_and_classes(ctx):
     """SteppingTest-style use of the operator mirror (SteppingTest.java:55-80)."""
     for w in jw.WaveletBuilder.create2arr():
