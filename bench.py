@@ -52,6 +52,8 @@ def parse(argv=None):
     p.add_argument("--workload", default="fwt1d", choices=WORKLOADS)
     p.add_argument("--math", default="exact", choices=["exact", "fma"])
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--config-cpu-seconds", type=float, default=3.0,
+                   help="CPU-leg budget of each config object in the default line")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-secondary", action="store_true",
                    help="skip the config-4 strong-scaling object of the default run")
@@ -558,13 +560,12 @@ def secondary_wpt(args, d):
     return out
 
 
-def _copy_threads():
-    """Threads of the library's host copy pool: the process's CPU share, at
-    most 16 (capi.cpp pin_ring)."""
+def _affinity():
+    """CPUs this process may run on (the box's share, not its nproc)."""
     try:
-        return min(len(os.sched_getaffinity(0)), 16)
+        return len(os.sched_getaffinity(0))
     except Exception:
-        return min(os.cpu_count() or 1, 16)
+        return os.cpu_count() or 1
 
 
 def host_entry(args, d, reps=5):
@@ -616,9 +617,12 @@ def host_entry(args, d, reps=5):
     # of the host copies that ran while a DMA was in flight
     cp = (st[0] + st[3]) / nst * 1e3
     wt = (st[1] + st[2]) / nst * 1e3
-    out["ring"] = {"copy_threads": _copy_threads(), "host_copy_ms_per_step": round(cp, 3),
-                   "dma_wait_ms_per_step": round(wt, 3),
-                   "bytes_per_step": (st[4] + st[5]) / nst}
+    nbytes = (st[4] + st[5]) / nst
+    out["ring"] = {"copy_threads": lib.jwv_host_copy_threads(),
+                   "host_copy_ms_per_step": round(cp, 3),
+                   "host_copy_GBps": round(nbytes / (cp * 1e-3) / 1e9, 1) if cp > 0 else None,
+                   "dma_wait_ms_per_step": round(wt, 3), "bytes_per_step": nbytes,
+                   "cpu_affinity": _affinity()}
     err = float(np.abs(xr - x).max())
     bufs = [ctypes.c_void_p() for _ in range(3)]
     try:
@@ -731,10 +735,11 @@ def kernels_of(prof):
 def secondary_configs(args, d):
     """BASELINE configs 3, 4 (EXACT and FMA) and 5 at one GPU, each timed as
     its own --workload run would time it (same warmup, regions A and B), in
-    compact form; no CPU legs (the per-workload runs carry those).  One
-    object per config, {"error": ...} if one fails."""
+    compact form.  One object per config, {"error": ...} if one fails.
+    Returns (objects, CPU-baseline specs): main() times the CPU legs after
+    every GPU leg."""
     import copy
-    out = {}
+    out, specs = {}, {}
     for key, wl, math in (("config3_fwt2d", "fwt2d", "exact"), ("config4_wpt", "wpt", "exact"),
                           ("config4_wpt_fma", "wpt", "fma"), ("config5_modwt", "modwt", "exact")):
         a = copy.copy(args)
@@ -752,12 +757,35 @@ def secondary_configs(args, d):
                  "roundtrip_max_abs_err": W["check"]()}
             if r["fp64"]:
                 o["roofline_fp64"] = r["fp64"]
+            specs[key] = W["cpu"]
             W["ctx"].close()
             del W
         except Exception as e:  # one config's failure must not void the metric line
             o = {"workload": wl, "math": math, "error": "%s: %s" % (type(e).__name__, e)}
         out[key] = o
-    return out
+    return out, specs
+
+
+def config_cpu_baselines(configs, specs, seconds):
+    """Bounded CPU legs of the driver-timed config objects (rank 0, after every
+    GPU leg): the same restated reference paths as cpu_baseline() -- config 3
+    on the full matrix over the host threads, config 4 on a 64-signal sample,
+    config 5 on the 131071-sample DIRECT prefix.  The FMA object shares config
+    4's leg: the reference has one CPU path for both."""
+    done = {}
+    for key, o in configs.items():
+        spec = specs.get(key)
+        if spec is None or "error" in o:
+            continue
+        wl = spec[0]
+        if wl in done:
+            o["cpu_baseline"] = dict(done[wl][1], same_as=done[wl][0])
+            continue
+        try:
+            o["cpu_baseline"] = cpu_baseline(spec, seconds)
+            done[wl] = (key, o["cpu_baseline"])
+        except Exception as e:
+            o["cpu_baseline"] = {"error": "%s: %s" % (type(e).__name__, e)}
 
 
 def main():
@@ -805,11 +833,13 @@ def main():
         # configs 3-5 at one GPU in the driver-timed line (their sharded
         # multi-GPU forms are --workload runs)
         if d.world == 1:
-            out["configs"] = secondary_configs(args, d)
+            out["configs"], cfg_specs = secondary_configs(args, d)
     # the reference's CPU path on this node's host cores, in the same run, at
     # every world size (rank 0, after every GPU leg)
     if d.rank == 0 and W["cpu"] and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(W["cpu"], args.cpu_seconds)
+        if "configs" in out:
+            config_cpu_baselines(out["configs"], cfg_specs, args.config_cpu_seconds)
     else:
         out["cpu_baseline"] = None
     if d.rank == 0:

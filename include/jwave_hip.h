@@ -149,6 +149,10 @@ int jwv_host_free(jwv_ctx* ctx, void* p);
  * of the ring, out[4] bytes staged in, out[5] bytes staged out.  reset != 0
  * zeroes them after reading.  Diagnostic (bench.py's host_entry object). */
 int jwv_ctx_stage_stats(jwv_ctx* ctx, double* out6, int reset);
+/* Threads of the process-wide host copy pool that stages pageable arrays
+ * (counting the calling thread): min(CPU affinity, 16) for single-device use,
+ * grown to min(CPU affinity, 16 x devices) by jwv_mctx_create. */
+int jwv_host_copy_threads(void);
 int jwv_version(void);
 
 /* ---- 1-D FWT ---------------------------------------------------------------

@@ -71,6 +71,7 @@ _SIGS = {
     "jwv_host_alloc": [_CTX, _i64, ctypes.POINTER(ctypes.c_void_p)],
     "jwv_host_free": [_CTX, ctypes.c_void_p],
     "jwv_ctx_stage_stats": [_CTX, ctypes.POINTER(ctypes.c_double), _int],
+    "jwv_host_copy_threads": [],
     "jwv_modwt_fwd_ld_f64_dev": [_dp, _dp, _i64, _i64, _int, _TP, _CTX],
     "jwv_modwt_inv_ld_f64_dev": [_dp, _i64, _dp, _i64, _int, _TP, _CTX],
     "jwv_ctx_profile_enable": [_CTX, _int],

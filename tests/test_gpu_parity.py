@@ -1293,7 +1293,12 @@ def test_host_entry_staging_paths(ctx):
             py = np.ctypeslib.as_array((ctypes.c_double * n).from_address(pin[1].value))
             px[:] = x
             dp = ctypes.POINTER(ctypes.c_double)
-            for src, dst in ((px, py), (px, np.empty(n)), (x, py)):
+            # pageable arrays 8 B off a 64-B line (the staging copies stream
+            # 64-B aligned stores after a memcpy head)
+            xo = np.empty(n + 3)[3:]
+            xo[:] = x
+            for src, dst in ((px, py), (px, np.empty(n)), (x, py), (xo, np.empty(n + 1)[1:]),
+                             (xo, py)):
                 dst[:] = np.nan
                 rc = lib.jwv_fwt_fwd_f64(src.ctypes.data_as(dp), dst.ctypes.data_as(dp), n, lev,
                                          t, ctx.handle)
