@@ -231,6 +231,39 @@ int jwv_m_wpt_fwd_batch_f64(const double* x, double* y, int64_t batch, int64_t n
                             int level, const jwv_taps* t, jwv_mctx* m);
 int jwv_m_wpt_rev_batch_f64(const double* y, double* x, int64_t batch, int64_t n, int64_t ld,
                             int level, const jwv_taps* t, jwv_mctx* m);
+/* ParallelTransform.forward / reverse(double[][], lvlM, lvlN)
+ * (ParallelTransform.java:70-126) over the listed devices: device i takes the
+ * row block [i rw, (i+1) rw) and, after one device-to-device exchange
+ * (hipMemcpyPeerAsync over xGMI), the column slab [i cw, (i+1) cw), rw =
+ * rows/D, cw = cols/D: forward = H2D row block, row pass straight into the
+ * exchange layout, exchange, column pass, D2H of the column slab into the host
+ * matrix's columns; reverse mirrors it.  D = the largest power of two <= the
+ * device count that divides rows with cw >= 2 (1: the single-device entry on
+ * device 0).  Host arrays as jwv_fwt2d_*_f64; results are that entry's bits.
+ * Distinct physical devices have not been measured on this project's 1-GPU
+ * pool (tests list device 0 twice). */
+int jwv_m_fwt2d_fwd_f64(const double* x, double* y, int64_t rows, int64_t cols, int lvl_m,
+                        int lvl_n, const jwv_taps* t, jwv_mctx* m);
+int jwv_m_fwt2d_rev_f64(const double* y, double* x, int64_t rows, int64_t cols, int lvl_m,
+                        int lvl_n, const jwv_taps* t, jwv_mctx* m);
+int jwv_m_wpt2d_fwd_f64(const double* x, double* y, int64_t rows, int64_t cols, int lvl_m,
+                        int lvl_n, const jwv_taps* t, jwv_mctx* m);
+int jwv_m_wpt2d_rev_f64(const double* y, double* x, int64_t rows, int64_t cols, int lvl_m,
+                        int lvl_n, const jwv_taps* t, jwv_mctx* m);
+/* MODWTTransform.forwardMODWT / inverseMODWT of `batch` signals of length n
+ * (MODWTTransform.java:256-375): x [batch][n], coefficients [batch][J+1][n]
+ * (each signal's double[J+1][n] packed).  jwv_modwt_*_batch_f64 on one
+ * device, signal after signal; jwv_m_*: contiguous blocks of signals per
+ * device (jwv_batch_split), one host thread per device.  Validation and
+ * messages are forwardMODWT's. */
+int jwv_modwt_fwd_batch_f64(const double* x, double* wv, int64_t batch, int64_t n, int J,
+                            const jwv_taps* t, jwv_ctx* ctx);
+int jwv_modwt_inv_batch_f64(const double* wv, double* x, int64_t batch, int64_t n, int J,
+                            const jwv_taps* t, jwv_ctx* ctx);
+int jwv_m_modwt_fwd_batch_f64(const double* x, double* wv, int64_t batch, int64_t n, int J,
+                              const jwv_taps* t, jwv_mctx* m);
+int jwv_m_modwt_inv_batch_f64(const double* wv, double* x, int64_t batch, int64_t n, int J,
+                              const jwv_taps* t, jwv_mctx* m);
 
 /* ---- 2-D / 3-D FWT -----------------------------------------------------------
  * BasicTransform.forward(double[][], lvlM, lvlN)  BasicTransform.java:361-399

@@ -367,3 +367,62 @@ JNIEXPORT jint JNICALL Java_jwave_amd_HipNative_transformBatchMulti(
                : jwv_m_wpt_rev_batch_f64(x, y, batch, n, n, level, t, MCTX(mctx));
   });
 }
+
+/* BasicTransform / ParallelTransform forward|reverse(double[][]) over the
+ * devices of a multi-context: row blocks, one device-to-device exchange,
+ * column slabs (jwv_m_{fwt,wpt}2d_*); staged once like transformBatchMulti */
+JNIEXPORT jint JNICALL Java_jwave_amd_HipNative_transform2dMulti(
+    JNIEnv* env, jclass cls, jlong mctx, jint kind, jboolean fwd, jdoubleArray jx,
+    jdoubleArray jy, jint rows, jint cols, jint lvlM, jint lvlN, jint L, jint tw, jdouble scale,
+    jdoubleArray jlo, jdoubleArray jhi, jdoubleArray jlor, jdoubleArray jhir) {
+  const int64_t tot = (int64_t)rows * cols;
+  const jlong ctx = (jlong)(intptr_t)jwv_mctx_ctx(MCTX(mctx), 0);
+  if (!ctx) {
+    throw_java(env, "java/lang/IllegalArgumentException", "jwave_hip_jni: no multi-context");
+    return STAGE_FAIL;
+  }
+  TAPS(B);
+  STAGED(jx, tot, jy, tot, {
+    if (kind == 0)
+      rc = fwd ? jwv_m_fwt2d_fwd_f64(x, y, rows, cols, lvlM, lvlN, t, MCTX(mctx))
+               : jwv_m_fwt2d_rev_f64(x, y, rows, cols, lvlM, lvlN, t, MCTX(mctx));
+    else
+      rc = fwd ? jwv_m_wpt2d_fwd_f64(x, y, rows, cols, lvlM, lvlN, t, MCTX(mctx))
+               : jwv_m_wpt2d_rev_f64(x, y, rows, cols, lvlM, lvlN, t, MCTX(mctx));
+  });
+}
+
+/* MODWTTransform.forwardMODWT / inverseMODWT of `batch` signals of length n:
+ * x [batch][n], wv [batch][J+1][n] (jwv_m_modwt_*_batch_f64: contiguous
+ * blocks of signals per device) */
+JNIEXPORT jint JNICALL Java_jwave_amd_HipNative_modwtBatchMulti(
+    JNIEnv* env, jclass cls, jlong mctx, jboolean fwd, jdoubleArray jx, jdoubleArray jwv,
+    jint batch, jint n, jint J, jint L, jint tw, jdoubleArray jlo, jdoubleArray jhi,
+    jdoubleArray jlor, jdoubleArray jhir) {
+  const jdouble scale = 1.0;
+  const int64_t nx = (int64_t)batch * n, nw = (int64_t)batch * (J + 1) * n;
+  const jlong ctx = (jlong)(intptr_t)jwv_mctx_ctx(MCTX(mctx), 0);
+  if (!ctx) {
+    throw_java(env, "java/lang/IllegalArgumentException", "jwave_hip_jni: no multi-context");
+    return STAGE_FAIL;
+  }
+  TAPS(B);
+  if (fwd) STAGED(jx, nx, jwv, nw, {
+    rc = jwv_m_modwt_fwd_batch_f64(x, y, batch, n, J, t, MCTX(mctx));
+  });
+  STAGED(jwv, nw, jx, nx, { rc = jwv_m_modwt_inv_batch_f64(x, y, batch, n, J, t, MCTX(mctx)); });
+}
+
+/* the same batch on this thread's device (jwv_modwt_*_batch_f64) */
+JNIEXPORT jint JNICALL Java_jwave_amd_HipNative_modwtBatch(
+    JNIEnv* env, jclass cls, jlong ctx, jboolean fwd, jdoubleArray jx, jdoubleArray jwv,
+    jint batch, jint n, jint J, jint L, jint tw, jdoubleArray jlo, jdoubleArray jhi,
+    jdoubleArray jlor, jdoubleArray jhir) {
+  const jdouble scale = 1.0;
+  const int64_t nx = (int64_t)batch * n, nw = (int64_t)batch * (J + 1) * n;
+  TAPS(B);
+  if (fwd) STAGED(jx, nx, jwv, nw, {
+    rc = jwv_modwt_fwd_batch_f64(x, y, batch, n, J, t, CTX(ctx));
+  });
+  STAGED(jwv, nw, jx, nx, { rc = jwv_modwt_inv_batch_f64(x, y, batch, n, J, t, CTX(ctx)); });
+}

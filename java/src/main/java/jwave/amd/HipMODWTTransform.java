@@ -49,4 +49,56 @@ public class HipMODWTTransform extends MODWTTransform {
     }
     return x;
   }
+
+  /**
+   * forwardMODWT of every signal (equal lengths), in one native call that
+   * spreads contiguous blocks of signals over the -Djwave.hip.devices GPUs
+   * (else this thread's device).  Each result is forwardMODWT(signals[i],
+   * maxLevel) bit for bit; the reference's checks (empty input, levels) run
+   * per signal through the single-signal path.
+   */
+  public double[ ][ ][ ] forwardMODWT( double[ ][ ] signals, int maxLevel ) {
+    int b = signals.length, n = b == 0 ? 0 : signals[ 0 ].length;
+    boolean native_ = _taps != null && b > 0 && n > 0 && maxLevel >= 0
+        && HipNative.fitsArray( (long)b * ( maxLevel + 1 ), n );
+    for( int i = 0; native_ && i < b; i++ )
+      native_ = signals[ i ] != null && signals[ i ].length == n;
+    if( !native_ ) {
+      double[ ][ ][ ] out = new double[ b ][ ][ ];
+      for( int i = 0; i < b; i++ )
+        out[ i ] = forwardMODWT( signals[ i ], maxLevel );
+      return out;
+    }
+    try {
+      return HipNative.modwtForwardBatch( _taps, signals, maxLevel );
+    } catch( JWaveException e ) {
+      throw new IllegalStateException( e.getMessage( ), e );
+    }
+  }
+
+  /** inverseMODWT of every signal's coefficients (equal shapes), one native call. */
+  public double[ ][ ] inverseMODWT( double[ ][ ][ ] coefficients ) {
+    int b = coefficients.length;
+    boolean native_ = _taps != null && b > 0 && coefficients[ 0 ] != null
+        && coefficients[ 0 ].length > 1;
+    int J = native_ ? coefficients[ 0 ].length - 1 : 0;
+    int n = native_ ? coefficients[ 0 ][ 0 ].length : 0;
+    native_ = native_ && n > 0 && HipNative.fitsArray( (long)b * ( J + 1 ), n );
+    for( int i = 0; native_ && i < b; i++ ) {
+      native_ = coefficients[ i ] != null && coefficients[ i ].length == J + 1;
+      for( int r = 0; native_ && r <= J; r++ )
+        native_ = coefficients[ i ][ r ] != null && coefficients[ i ][ r ].length == n;
+    }
+    if( !native_ ) {
+      double[ ][ ] out = new double[ b ][ ];
+      for( int i = 0; i < b; i++ )
+        out[ i ] = inverseMODWT( coefficients[ i ] );
+      return out;
+    }
+    try {
+      return HipNative.modwtInverseBatch( _taps, coefficients );
+    } catch( JWaveException e ) {
+      throw new IllegalStateException( e.getMessage( ), e );
+    }
+  }
 }

@@ -175,6 +175,20 @@ public final class HipNative {
       double[ ] y, int batch, int n, int level, int L, int tw, double scale, double[ ] lo,
       double[ ] hi, double[ ] loR, double[ ] hiR );
 
+  /** transform2d over the devices of a multi-context (jwv_m_{fwt,wpt}2d_*):
+   *  row blocks, one device-to-device exchange, column slabs. */
+  static native int transform2dMulti( long mctx, int kind, boolean forward, double[ ] x,
+      double[ ] y, int rows, int cols, int lvlM, int lvlN, int L, int tw, double scale,
+      double[ ] lo, double[ ] hi, double[ ] loR, double[ ] hiR );
+
+  /** forwardMODWT / inverseMODWT of `batch` signals: x = batch*n, wv =
+   *  batch*(J+1)*n (jwv_m_modwt_*_batch_f64 / jwv_modwt_*_batch_f64). */
+  static native int modwtBatchMulti( long mctx, boolean forward, double[ ] x, double[ ] wv,
+      int batch, int n, int J, int L, int tw, double[ ] lo, double[ ] hi, double[ ] loR,
+      double[ ] hiR );
+  static native int modwtBatch( long ctx, boolean forward, double[ ] x, double[ ] wv, int batch,
+      int n, int J, int L, int tw, double[ ] lo, double[ ] hi, double[ ] loR, double[ ] hiR );
+
   /** batch signals of length n, packed contiguously (ld = n). */
   static native int transformBatch( long ctx, int kind, boolean forward, double[ ] x,
       double[ ] y, int batch, int n, int level, int L, int tw, double scale, double[ ] lo,
@@ -234,14 +248,60 @@ public final class HipNative {
     return fitsArray( P * Q, R );
   }
 
-  /** BasicTransform.forward|reverse(double[][], lvlM, lvlN) in one call. */
+  /** BasicTransform.forward|reverse(double[][], lvlM, lvlN) in one call: over
+   *  the jwave.hip.devices GPUs when set (row blocks, one device-to-device
+   *  exchange, column slabs: ParallelTransform.java:70-126's split), else on
+   *  this thread's device.  The same bits either way. */
   static double[ ][ ] run2d( int kind, Taps t, boolean fwd, double[ ][ ] m, int lvlM, int lvlN )
       throws JWaveException {
     int rows = m.length, cols = rows == 0 ? 0 : m[ 0 ].length;
     double[ ] x = pack( m ), y = new double[ x.length ];
-    check( transform2d( ctx( ), kind, fwd, x, y, rows, cols, lvlM, lvlN, t.L, t.tw, t.scale,
-        t.lo, t.hi, t.loR, t.hiR ) );
+    long mc = mctx( );
+    if( mc != 0L )
+      checkMulti( mc, transform2dMulti( mc, kind, fwd, x, y, rows, cols, lvlM, lvlN, t.L, t.tw,
+          t.scale, t.lo, t.hi, t.loR, t.hiR ) );
+    else
+      check( transform2d( ctx( ), kind, fwd, x, y, rows, cols, lvlM, lvlN, t.L, t.tw, t.scale,
+          t.lo, t.hi, t.loR, t.hiR ) );
     return unpack( y, rows, cols );
+  }
+
+  /** forwardMODWT of every signal (equal lengths) in one native call: over
+   *  the jwave.hip.devices GPUs when set, else this thread's device.
+   *  Returns [signal][level row][n]. */
+  static double[ ][ ][ ] modwtForwardBatch( Taps t, double[ ][ ] signals, int J )
+      throws JWaveException {
+    int b = signals.length, n = b == 0 ? 0 : signals[ 0 ].length;
+    double[ ] x = pack( signals ), wv = new double[ b * ( J + 1 ) * n ];
+    long mc = mctx( );
+    if( mc != 0L )
+      checkMulti( mc, modwtBatchMulti( mc, true, x, wv, b, n, J, t.L, t.tw, t.lo, t.hi, t.loR,
+          t.hiR ) );
+    else
+      check( modwtBatch( ctx( ), true, x, wv, b, n, J, t.L, t.tw, t.lo, t.hi, t.loR, t.hiR ) );
+    double[ ][ ][ ] out = new double[ b ][ ][ ];
+    for( int i = 0; i < b; i++ ) {
+      out[ i ] = new double[ J + 1 ][ n ];
+      for( int r = 0; r <= J; r++ )
+        System.arraycopy( wv, ( i * ( J + 1 ) + r ) * n, out[ i ][ r ], 0, n );
+    }
+    return out;
+  }
+
+  /** inverseMODWT of every signal's [J+1][n] coefficients in one native call. */
+  static double[ ][ ] modwtInverseBatch( Taps t, double[ ][ ][ ] c ) throws JWaveException {
+    int b = c.length, J = c[ 0 ].length - 1, n = c[ 0 ][ 0 ].length;
+    double[ ] wv = new double[ b * ( J + 1 ) * n ], x = new double[ b * n ];
+    for( int i = 0; i < b; i++ )
+      for( int r = 0; r <= J; r++ )
+        System.arraycopy( c[ i ][ r ], 0, wv, ( i * ( J + 1 ) + r ) * n, n );
+    long mc = mctx( );
+    if( mc != 0L )
+      checkMulti( mc, modwtBatchMulti( mc, false, x, wv, b, n, J, t.L, t.tw, t.lo, t.hi, t.loR,
+          t.hiR ) );
+    else
+      check( modwtBatch( ctx( ), false, x, wv, b, n, J, t.L, t.tw, t.lo, t.hi, t.loR, t.hiR ) );
+    return unpack( x, b, n );
   }
 
   /** BasicTransform.forward|reverse(double[][][], lvlP, lvlQ, lvlR) in one

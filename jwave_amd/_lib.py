@@ -125,6 +125,11 @@ _SIGS.update({
 })
 for _n in ("fwt_fwd", "fwt_rev", "wpt_fwd", "wpt_rev"):
     _SIGS["jwv_m_%s_batch_f64" % _n] = [_dp, _dp, _i64, _i64, _i64, _int, _TP, _MCTX]
+for _n in ("fwt2d_fwd", "fwt2d_rev", "wpt2d_fwd", "wpt2d_rev"):
+    _SIGS["jwv_m_%s_f64" % _n] = [_dp, _dp, _i64, _i64, _int, _int, _TP, _MCTX]
+for _n in ("modwt_fwd", "modwt_inv"):
+    _SIGS["jwv_%s_batch_f64" % _n] = [_dp, _dp, _i64, _i64, _int, _TP, _CTX]
+    _SIGS["jwv_m_%s_batch_f64" % _n] = [_dp, _dp, _i64, _i64, _int, _TP, _MCTX]
 
 _RESTYPES = {"jwv_last_error": ctypes.c_char_p, "jwv_ctx_get_stream": ctypes.c_void_p,
              "jwv_mctx_last_error": ctypes.c_char_p, "jwv_mctx_ctx": ctypes.c_void_p}

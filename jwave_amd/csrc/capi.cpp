@@ -142,11 +142,33 @@ class CopyPool {
       const size_t off = per * i;
       if (off >= bytes) break;
       ++g.pending;
-      jobs_.push_back({&g, (char*)dst + off, (const char*)src + off, std::min(per, bytes - off)});
+      jobs_.push_back({&g, (char*)dst + off, (const char*)src + off, std::min(per, bytes - off),
+                       0, 0, 1});
     }
     lk.unlock();
     cv_.notify_all();
     nt_copy(dst, src, std::min(per, bytes));
+    lk.lock();
+    done_.wait(lk, [&g] { return g.pending == 0; });
+  }
+  // nrows rows of w bytes, at pitches dp / sp bytes; rows split over the pool
+  void copy2d(void* dst, size_t dp, const void* src, size_t sp, size_t w, size_t nrows) {
+    const size_t bytes = w * nrows;
+    const int parts = (int)std::min<size_t>(bytes >= (size_t(1) << 20) ? size() : 1, nrows);
+    const size_t per = (nrows + parts - 1) / parts;
+    Group g;
+    std::unique_lock<std::mutex> lk(mu_);
+    for (int i = 1; i < parts; ++i) {
+      const size_t r0 = per * i;
+      if (r0 >= nrows) break;
+      ++g.pending;
+      jobs_.push_back({&g, (char*)dst + r0 * dp, (const char*)src + r0 * sp, w, dp, sp,
+                       std::min(per, nrows - r0)});
+    }
+    lk.unlock();
+    cv_.notify_all();
+    for (size_t r = 0; r < std::min(per, nrows); ++r)
+      nt_copy((char*)dst + r * dp, (const char*)src + r * sp, w);
     lk.lock();
     done_.wait(lk, [&g] { return g.pending == 0; });
   }
@@ -159,7 +181,8 @@ class CopyPool {
     Group* g;
     char* d;
     const char* s;
-    size_t n;
+    size_t n;            // bytes per row
+    size_t dp, sp, rows; // row pitches (bytes) and row count (1: one contiguous run)
   };
   void loop() {
     std::unique_lock<std::mutex> lk(mu_);
@@ -168,7 +191,7 @@ class CopyPool {
       const Job job = jobs_.front();
       jobs_.pop_front();
       lk.unlock();
-      nt_copy(job.d, job.s, job.n);
+      for (size_t r = 0; r < job.rows; ++r) nt_copy(job.d + r * job.dp, job.s + r * job.sp, job.n);
       lk.lock();
       if (--job.g->pending == 0) done_.notify_all();
     }
@@ -241,6 +264,10 @@ struct jwv_mctx {
   std::vector<jwv_ctx*> ctx;  // one per listed device
   std::string err;
   std::mutex mu;
+  // multi-device 2-D (jwv_m_fwt2d_*): per device three block buffers, a
+  // packing scratch, and the event that ends its first phase
+  std::vector<DevBuf> a, b, c, t;
+  std::vector<hipEvent_t> ev;
 };
 
 namespace {
@@ -1118,6 +1145,93 @@ void copy_out(jwv_ctx* c, const double* dy, double* y, size_t n) {
     if (k + kPinSlots < nk) issue(k + kPinSlots);
   }
   r.stat[5] += (double)bytes;
+  hipchk(hipStreamSynchronize(c->stream), "sync");
+}
+
+// Row-strided host side (a column slab of a row-major host matrix): nrows
+// rows of w doubles at a pitch of `pitch` doubles <-> a contiguous [nrows][w]
+// device block.  Same pinned ring and ramped ends as copy_in / copy_out, in
+// whole rows per chunk.
+std::vector<Chunk> stage_row_chunks(size_t nrows, size_t w, bool ramp_up) {
+  const size_t rb = w * sizeof(double);
+  const size_t full = std::max<size_t>(1, kPinChunk / rb);
+  size_t want = std::max<size_t>(1, full >> 3), left = nrows;
+  std::vector<size_t> len;
+  while (left > 0) {
+    const size_t l = std::min(left, want);
+    len.push_back(l);
+    left -= l;
+    want = std::min(full, want * 2);
+  }
+  if (!ramp_up) std::reverse(len.begin(), len.end());
+  std::vector<Chunk> out;
+  size_t r0 = 0;
+  for (size_t l : len) {
+    out.push_back({r0, l});
+    r0 += l;
+  }
+  return out;
+}
+void copy_in2d(jwv_ctx* c, const double* x, size_t pitch, size_t nrows, size_t w, double* dx) {
+  const size_t rb = w * sizeof(double);
+  if (host_pinned(x)) {
+    hipchk(hipMemcpy2DAsync(dx, rb, x, pitch * sizeof(double), rb, nrows, hipMemcpyHostToDevice,
+                            c->stream), "H2D 2D");
+    return;
+  }
+  if (rb > kPinChunk) {  // rows longer than a slot: row by row
+    for (size_t r = 0; r < nrows; ++r) copy_in(c, x + r * pitch, dx + r * w, w);
+    return;
+  }
+  PinRing& r = pin_ring(c);
+  const std::vector<Chunk> ch = stage_row_chunks(nrows, w, true);
+  for (size_t k = 0; k < ch.size(); ++k) {
+    const int s = (int)(k % kPinSlots);
+    const double t0 = now_s();
+    hipchk(hipEventSynchronize(r.ev[s]), "staging slot");
+    const double t1 = now_s();
+    copy_pool().copy2d(r.p[s], rb, x + ch[k].off * pitch, pitch * sizeof(double), rb, ch[k].len);
+    r.stat[1] += t1 - t0;
+    r.stat[0] += now_s() - t1;
+    hipchk(hipMemcpyAsync(dx + ch[k].off * w, r.p[s], ch[k].len * rb, hipMemcpyHostToDevice,
+                          c->stream), "H2D");
+    hipchk(hipEventRecord(r.ev[s], c->stream), "hipEventRecord");
+  }
+  r.stat[4] += (double)(rb * nrows);
+}
+void copy_out2d(jwv_ctx* c, const double* dy, size_t nrows, size_t w, double* y, size_t pitch) {
+  const size_t rb = w * sizeof(double);
+  if (host_pinned(y)) {
+    hipchk(hipMemcpy2DAsync(y, pitch * sizeof(double), dy, rb, rb, nrows, hipMemcpyDeviceToHost,
+                            c->stream), "D2H 2D");
+    hipchk(hipStreamSynchronize(c->stream), "sync");
+    return;
+  }
+  if (rb > kPinChunk) {
+    for (size_t r = 0; r < nrows; ++r) copy_out(c, dy + r * w, y + r * pitch, w);
+    return;
+  }
+  PinRing& r = pin_ring(c);
+  const std::vector<Chunk> ch = stage_row_chunks(nrows, w, false);
+  const size_t nk = ch.size();
+  auto issue = [&](size_t k) {
+    const int s = (int)(k % kPinSlots);
+    hipchk(hipMemcpyAsync(r.p[s], dy + ch[k].off * w, ch[k].len * rb, hipMemcpyDeviceToHost,
+                          c->stream), "D2H");
+    hipchk(hipEventRecord(r.ev[s], c->stream), "hipEventRecord");
+  };
+  for (size_t k = 0; k < std::min<size_t>(nk, kPinSlots); ++k) issue(k);
+  for (size_t k = 0; k < nk; ++k) {
+    const int s = (int)(k % kPinSlots);
+    const double t0 = now_s();
+    hipchk(hipEventSynchronize(r.ev[s]), "staging slot");
+    const double t1 = now_s();
+    copy_pool().copy2d(y + ch[k].off * pitch, pitch * sizeof(double), r.p[s], rb, rb, ch[k].len);
+    r.stat[2] += t1 - t0;
+    r.stat[3] += now_s() - t1;
+    if (k + kPinSlots < nk) issue(k + kPinSlots);
+  }
+  r.stat[5] += (double)(rb * nrows);
   hipchk(hipStreamSynchronize(c->stream), "sync");
 }
 
@@ -2212,6 +2326,22 @@ int jwv_mctx_create(const int* devices, int n, jwv_mctx** out) {
   // one staging thread per device shares the process-wide copy pool: size it
   // by the devices in use (16 threads each, within the CPU share)
   copy_pool().grow(std::min(affinity_cpus(), 16 * n) - 1);
+  // direct xGMI peer copies for the 2-D exchange where the pair allows it
+  // (otherwise hipMemcpyPeerAsync stages through the host)
+  int prev = -1;
+  if (hipGetDevice(&prev) == hipSuccess) {
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < n; ++j) {
+        int can = 0;
+        if (devices[i] == devices[j] ||
+            hipDeviceCanAccessPeer(&can, devices[i], devices[j]) != hipSuccess || !can)
+          continue;
+        if (hipSetDevice(devices[i]) == hipSuccess &&
+            hipDeviceEnablePeerAccess(devices[j], 0) != hipSuccess)
+          (void)hipGetLastError();  // already enabled
+      }
+    (void)hipSetDevice(prev);
+  }
   *out = m;
   return JWV_OK;
 }
@@ -2220,6 +2350,16 @@ int jwv_host_copy_threads(void) { return copy_pool().size(); }
 
 int jwv_mctx_destroy(jwv_mctx* m) {
   if (!m) return JWV_OK;
+  int prev = -1;
+  if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  for (size_t i = 0; i < m->a.size(); ++i) {
+    if (hipSetDevice(m->ctx[i]->device) != hipSuccess) continue;
+    (void)hipStreamSynchronize(m->ctx[i]->stream);
+    for (DevBuf* d : {&m->a[i], &m->b[i], &m->c[i], &m->t[i]})
+      if (d->p) (void)hipFree(d->p);
+    if (m->ev[i]) (void)hipEventDestroy(m->ev[i]);
+  }
+  if (prev >= 0) (void)hipSetDevice(prev);
   for (jwv_ctx* c : m->ctx) jwv_ctx_destroy(c);
   delete m;
   return JWV_OK;
@@ -2294,5 +2434,270 @@ JWV_MBATCH(jwv_m_fwt_fwd_batch_f64, jwv_fwt_fwd_batch_f64, Kind::FWT, true)
 JWV_MBATCH(jwv_m_fwt_rev_batch_f64, jwv_fwt_rev_batch_f64, Kind::FWT, false)
 JWV_MBATCH(jwv_m_wpt_fwd_batch_f64, jwv_wpt_fwd_batch_f64, Kind::WPT, true)
 JWV_MBATCH(jwv_m_wpt_rev_batch_f64, jwv_wpt_rev_batch_f64, Kind::WPT, false)
+
+// ---- multi-device 2-D ------------------------------------------------------------
+// ParallelTransform.forward / reverse(double[][]) (ParallelTransform.java:70-126:
+// rows split over threads, join, columns split over threads) over D GPUs of one
+// process.  Device i holds rows [i rw, (i+1) rw) and, after one exchange,
+// columns [i cw, (i+1) cw) (rw = rows/D, cw = cols/D):
+//   forward  H2D row block -> row pass writing the exchange layout [D][rw][cw]
+//            (jwv_fwt_rows_seg_*) -> every device pulls chunk i of every
+//            device's block (hipMemcpyPeerAsync, xGMI; each waits on the
+//            owners' phase-1 events) -> the received [rows][cw] slab's column
+//            pass -> D2H into the columns of the host matrix (row-strided).
+//   reverse  H2D column slab (row-strided) -> column pass -> exchange -> row
+//            pass reading the chunks -> D2H of the row block.
+// Each device's PCIe link carries 1/D of the bytes, each of its host copies
+// runs on the process pool (grown to 16 threads per device).  D is the
+// largest power of two <= the listed devices that divides rows with cw >= 2;
+// 1 runs the single-device entry on the first device.  Results are the
+// single-device entries' bits: the row and column passes are the same kernels
+// on the same lines in the same order.
+namespace {
+class HostBarrier {
+ public:
+  explicit HostBarrier(int n) : n_(n) {}
+  void wait() {
+    std::unique_lock<std::mutex> lk(mu_);
+    const int g = gen_;
+    if (++count_ == n_) {
+      count_ = 0;
+      ++gen_;
+      cv_.notify_all();
+      return;
+    }
+    cv_.wait(lk, [&] { return gen_ != g; });
+  }
+
+ private:
+  int n_, count_ = 0, gen_ = 0;
+  std::mutex mu_;
+  std::condition_variable cv_;
+};
+
+int m2d_devices(int D, int64_t rows, int64_t cols) {
+  int d = 1;
+  while (d * 2 <= D) d *= 2;
+  while (d > 1 && (rows % d || cols % d || cols / d < 2)) d /= 2;
+  return d;
+}
+
+// row pass of `rows` rows into the exchange layout [cols/seg][rows][seg]
+void rows_to_chunks(jwv_ctx* c, Kind k, const Bank& b, const double* x, double* y, int64_t rows,
+                    int64_t cols, int level, int64_t seg, DevBuf& tmp) {
+  const AxisView rv = cview(cols, 1);
+  if (k == Kind::FWT) {
+    AxisView ov = rv;
+    ov.s_outer = seg;
+    Axis a{x, rv, y, ov, rows, (int)cols, 1};
+    a.lsw = exponent(seg);
+    a.ss = rows * seg;
+    Plan p = fwt_fwd_plan(c, b, a, level, c->ws);
+    if (!p.empty()) return run_plan(p);
+  }
+  double* t = grow(c, tmp, (size_t)(rows * cols));
+  axis_fn(k, true)(c, b, Axis{x, rv, t, rv, rows, (int)cols, 1}, level);
+  copy_axis(c, seg_pack_axis(t, y, rows, cols, seg, true));
+}
+// reverse row pass reading the exchange layout
+void chunks_to_rows(jwv_ctx* c, Kind k, const Bank& b, const double* y, double* x, int64_t rows,
+                    int64_t cols, int level, int64_t seg, DevBuf& tmp) {
+  const AxisView rv = cview(cols, 1);
+  if (k == Kind::FWT) {
+    AxisView iv = rv;
+    iv.s_outer = seg;
+    Axis a{y, iv, x, rv, rows, (int)cols, 1};
+    a.lsw = exponent(seg);
+    a.ss = rows * seg;
+    Plan p = fwt_rev_plan(c, b, a, level, c->ws);
+    if (!p.empty()) return run_plan(p);
+  }
+  double* t = grow(c, tmp, (size_t)(rows * cols));
+  copy_axis(c, seg_pack_axis(t, const_cast<double*>(y), rows, cols, seg, false));
+  axis_fn(k, false)(c, b, Axis{t, rv, x, rv, rows, (int)cols, 1}, level);
+}
+
+using Single2d = int (*)(const double*, double*, int64_t, int64_t, int, int, const jwv_taps*,
+                         jwv_ctx*);
+int m2d(Kind k, bool fwd, Single2d single, const double* in, double* out, int64_t rows,
+        int64_t cols, int lvl_m, int lvl_n, const jwv_taps* t, jwv_mctx* m) {
+  if (!m) return set_err(nullptr, JWV_ERR_BAD_CALL, "jwv_mctx is NULL");
+  std::lock_guard<std::mutex> lk(m->mu);
+  m->err.clear();
+  Bank b;
+  try {  // once, with the single-device entries' checks and messages
+    b = make_bank(t);
+    check_2d(k, fwd, rows, cols, lvl_m, lvl_n);
+    if (rows == 0 || cols == 0) return JWV_OK;
+    check_ptrs(in, out);
+  } catch (const Fail& e) {
+    m->err = e.msg;
+    return e.code;
+  }
+  const int D = m2d_devices((int)m->ctx.size(), rows, cols);
+  if (D == 1) {
+    const int rc = single(in, out, rows, cols, lvl_m, lvl_n, t, m->ctx[0]);
+    if (rc != JWV_OK) m->err = jwv_last_error(m->ctx[0]);
+    return rc;
+  }
+  const size_t nd = m->ctx.size();
+  if (m->a.size() < nd) {
+    m->a.resize(nd), m->b.resize(nd), m->c.resize(nd), m->t.resize(nd);
+    m->ev.resize(nd, nullptr);
+  }
+  const int64_t rw = rows / D, cw = cols / D;
+  const size_t blk = (size_t)(rw * cols), chunk = (size_t)(rw * cw);
+  std::vector<int> rc1(D, JWV_OK), rc2(D, JWV_OK);
+  HostBarrier bar(D);
+  auto work = [&](int i) {
+    jwv_ctx* c = m->ctx[i];
+    const AxisView sv = cview(rows, cw);  // a [rows][cw] slab, lines along rows
+    rc1[i] = guarded(c, [&] {
+      double* A = grow(c, m->a[i], blk);
+      double* B = grow(c, m->b[i], blk);
+      if (fwd) {
+        copy_in(c, in + i * blk, A, blk);
+        rows_to_chunks(c, k, b, A, B, rw, cols, lvl_n, cw, m->c[i]);
+      } else {
+        copy_in2d(c, in + i * cw, (size_t)cols, (size_t)rows, (size_t)cw, A);
+        axis_fn(k, false)(c, b, Axis{A, sv, B, sv, 1, (int)rows, (int)cw}, lvl_m);
+      }
+      if (!m->ev[i]) HIPCHK(hipEventCreateWithFlags(&m->ev[i], hipEventDisableTiming));
+      HIPCHK(hipEventRecord(m->ev[i], c->stream));
+    });
+    bar.wait();  // every device's phase-1 work is queued (or has failed)
+    for (int d = 0; d < D; ++d)
+      if (rc1[d] != JWV_OK) return;
+    rc2[i] = guarded(c, [&] {
+      double* A = m->a[i].p;
+      double* C = grow(c, m->c[i], blk);
+      // chunk i of every device's exchange block -> my slab (forward) / row
+      // block's chunks (reverse)
+      for (int d = 0; d < D; ++d) {
+        HIPCHK(hipStreamWaitEvent(c->stream, m->ev[d], 0));
+        HIPCHK(hipMemcpyPeerAsync(A + d * chunk, c->device, m->b[d].p + i * chunk,
+                                  m->ctx[d]->device, chunk * sizeof(double), c->stream));
+      }
+      if (fwd) {
+        axis_fn(k, true)(c, b, Axis{A, sv, C, sv, 1, (int)rows, (int)cw}, lvl_m);
+        copy_out2d(c, C, (size_t)rows, (size_t)cw, out + i * cw, (size_t)cols);
+      } else {
+        chunks_to_rows(c, k, b, A, C, rw, cols, lvl_n, cw, m->t[i]);
+        copy_out(c, C, out + i * blk, blk);
+      }
+      check_waits(c);
+    });
+  };
+  std::vector<std::thread> th;
+  for (int i = 1; i < D; ++i) th.emplace_back(work, i);
+  work(0);
+  for (auto& h : th) h.join();
+  for (auto* rc : {&rc1, &rc2})
+    for (int i = 0; i < D; ++i)
+      if ((*rc)[i] != JWV_OK) {
+        m->err = "device " + std::to_string(m->ctx[i]->device) + ": " + jwv_last_error(m->ctx[i]);
+        return (*rc)[i];
+      }
+  return JWV_OK;
+}
+}  // namespace
+
+int jwv_m_fwt2d_fwd_f64(const double* x, double* y, int64_t rows, int64_t cols, int lvl_m,
+                        int lvl_n, const jwv_taps* t, jwv_mctx* m) {
+  return m2d(Kind::FWT, true, jwv_fwt2d_fwd_f64, x, y, rows, cols, lvl_m, lvl_n, t, m);
+}
+int jwv_m_fwt2d_rev_f64(const double* y, double* x, int64_t rows, int64_t cols, int lvl_m,
+                        int lvl_n, const jwv_taps* t, jwv_mctx* m) {
+  return m2d(Kind::FWT, false, jwv_fwt2d_rev_f64, y, x, rows, cols, lvl_m, lvl_n, t, m);
+}
+int jwv_m_wpt2d_fwd_f64(const double* x, double* y, int64_t rows, int64_t cols, int lvl_m,
+                        int lvl_n, const jwv_taps* t, jwv_mctx* m) {
+  return m2d(Kind::WPT, true, jwv_wpt2d_fwd_f64, x, y, rows, cols, lvl_m, lvl_n, t, m);
+}
+int jwv_m_wpt2d_rev_f64(const double* y, double* x, int64_t rows, int64_t cols, int lvl_m,
+                        int lvl_n, const jwv_taps* t, jwv_mctx* m) {
+  return m2d(Kind::WPT, false, jwv_wpt2d_rev_f64, y, x, rows, cols, lvl_m, lvl_n, t, m);
+}
+
+// ---- MODWT batches -----------------------------------------------------------------
+// forwardMODWT / inverseMODWT of `batch` signals of length n: x [batch][n],
+// coefficients [batch][J+1][n] (each signal's double[J+1][n], packed).  One
+// device: the signals one after another through the single-signal plan.
+// jwv_m_*: contiguous blocks of signals per device (jwv_batch_split), one
+// host thread per device, as the FWT/WPT batches.
+int jwv_modwt_fwd_batch_f64(const double* x, double* wv, int64_t batch, int64_t n, int J,
+                            const jwv_taps* t, jwv_ctx* c) {
+  return guarded(c, [&] {
+    const Bank b = make_bank(t);
+    if (batch < 0) throw Fail{JWV_ERR_BAD_CALL, "batch < 0"};
+    check_modwt(n, J);
+    if (n == 0 || batch == 0) return;
+    check_ptrs(x, wv);
+    const int64_t out = (int64_t)(J + 1) * n;
+    for (int64_t s = 0; s < batch; ++s)
+      staged(c, x + s * n, (size_t)n, wv + s * out, (size_t)out,
+             [&](const double* dx, double* dy) { body_modwt_fwd(c, b, dx, dy, n, J, n); });
+  });
+}
+int jwv_modwt_inv_batch_f64(const double* wv, double* x, int64_t batch, int64_t n, int J,
+                            const jwv_taps* t, jwv_ctx* c) {
+  return guarded(c, [&] {
+    const Bank b = make_bank(t);
+    if (batch < 0) throw Fail{JWV_ERR_BAD_CALL, "batch < 0"};
+    if (J < 1 || n == 0 || batch == 0) return;
+    check_ptrs(wv, x);
+    const int64_t in = (int64_t)(J + 1) * n;
+    for (int64_t s = 0; s < batch; ++s)
+      staged(c, wv + s * in, (size_t)in, x + s * n, (size_t)n,
+             [&](const double* dx, double* dy) { body_modwt_inv(c, b, dx, dy, n, J, n); });
+  });
+}
+namespace {
+using ModwtBatchFn = int (*)(const double*, double*, int64_t, int64_t, int, const jwv_taps*,
+                             jwv_ctx*);
+int mmodwt(bool fwd, ModwtBatchFn fn, const double* in, double* out, int64_t batch, int64_t n,
+           int J, const jwv_taps* t, jwv_mctx* m) {
+  if (!m) return set_err(nullptr, JWV_ERR_BAD_CALL, "jwv_mctx is NULL");
+  std::lock_guard<std::mutex> lk(m->mu);
+  m->err.clear();
+  try {
+    (void)make_bank(t);
+    if (batch < 0) throw Fail{JWV_ERR_BAD_CALL, "batch < 0"};
+    if (fwd) check_modwt(n, J);
+    if (n == 0 || batch == 0 || J < 1) return JWV_OK;
+    check_ptrs(in, out);
+  } catch (const Fail& e) {
+    m->err = e.msg;
+    return e.code;
+  }
+  const int64_t big = (int64_t)(J + 1) * n;
+  const int64_t sin = fwd ? n : big, sout = fwd ? big : n;
+  const int D = (int)m->ctx.size();
+  std::vector<int> rc(D, JWV_OK);
+  auto work = [&](int i) {
+    int64_t s0 = 0, cnt = 0;
+    jwv_batch_split(batch, D, i, &s0, &cnt);
+    if (cnt > 0) rc[i] = fn(in + s0 * sin, out + s0 * sout, cnt, n, J, t, m->ctx[i]);
+  };
+  std::vector<std::thread> th;
+  for (int i = 1; i < D; ++i) th.emplace_back(work, i);
+  work(0);
+  for (auto& h : th) h.join();
+  for (int i = 0; i < D; ++i)
+    if (rc[i] != JWV_OK) {
+      m->err = "device " + std::to_string(m->ctx[i]->device) + ": " + jwv_last_error(m->ctx[i]);
+      return rc[i];
+    }
+  return JWV_OK;
+}
+}  // namespace
+int jwv_m_modwt_fwd_batch_f64(const double* x, double* wv, int64_t batch, int64_t n, int J,
+                              const jwv_taps* t, jwv_mctx* m) {
+  return mmodwt(true, jwv_modwt_fwd_batch_f64, x, wv, batch, n, J, t, m);
+}
+int jwv_m_modwt_inv_batch_f64(const double* wv, double* x, int64_t batch, int64_t n, int J,
+                              const jwv_taps* t, jwv_mctx* m) {
+  return mmodwt(false, jwv_modwt_inv_batch_f64, wv, x, batch, n, J, t, m);
+}
 
 }  // extern "C"

@@ -187,6 +187,45 @@ class MultiContext:
                                              t, self.handle))
         return y
 
+    def transform_2d(self, x, wavelet, lvl_m, lvl_n, forward=True, kind="fwt"):
+        """ParallelTransform.forward / reverse(double[][], lvlM, lvlN) of the host
+        matrix x over the devices: row blocks, one device-to-device exchange,
+        column slabs (jwv_m_fwt2d_*); the single-device entry's bits."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        if x.ndim != 2:
+            raise JWaveFailure("MultiContext.transform_2d: a 2-D array is required")
+        rows, cols = x.shape
+        y = np.empty_like(x)
+        name = "jwv_m_%s2d_%s_f64" % (kind, "fwd" if forward else "rev")
+        self._check(getattr(self._lib, name)(x.ctypes.data, y.ctypes.data, rows, cols,
+                                             int(lvl_m), int(lvl_n), _TapsHolder.of(wavelet),
+                                             self.handle))
+        return y
+
+    def modwt_forward(self, x, wavelet, J):
+        """forwardMODWT of every row of x (batch x n) -> [batch][J+1][n]."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        if x.ndim != 2:
+            raise JWaveFailure("MultiContext.modwt_forward: a 2-D array of signals is required")
+        b, n = x.shape
+        c = np.empty((b, int(J) + 1, n))
+        self._check(self._lib.jwv_m_modwt_fwd_batch_f64(x.ctypes.data, c.ctypes.data, b, n,
+                                                        int(J), _TapsHolder.of(wavelet),
+                                                        self.handle))
+        return c
+
+    def modwt_inverse(self, c, wavelet):
+        """inverseMODWT of every [J+1][n] block of c ([batch][J+1][n])."""
+        c = np.ascontiguousarray(c, dtype=np.float64)
+        if c.ndim != 3:
+            raise JWaveFailure("MultiContext.modwt_inverse: [batch][J+1][n] coefficients required")
+        b, J1, n = c.shape
+        x = np.empty((b, n))
+        self._check(self._lib.jwv_m_modwt_inv_batch_f64(c.ctypes.data, x.ctypes.data, b, n,
+                                                        J1 - 1, _TapsHolder.of(wavelet),
+                                                        self.handle))
+        return x
+
     def close(self):
         if getattr(self, "handle", None):
             self._lib.jwv_mctx_destroy(self.handle)

@@ -174,3 +174,30 @@ TM(jwv_m_fwt_fwd_batch_f64, 30)
 TM(jwv_m_fwt_rev_batch_f64, 31)
 TM(jwv_m_wpt_fwd_batch_f64, 32)
 TM(jwv_m_wpt_rev_batch_f64, 33)
+#define TM2(NAME, K)                                                                  \
+  int NAME(const double* x, double* y, int64_t r, int64_t cl, int lm, int ln,         \
+           const jwv_taps* t, jwv_mctx* m) {                                         \
+    return rec(#NAME, x, r * cl, y, r * cl, K, t, r, cl, lm, ln, m->n, 0);           \
+  }
+TM2(jwv_m_fwt2d_fwd_f64, 34)
+TM2(jwv_m_fwt2d_rev_f64, 35)
+TM2(jwv_m_wpt2d_fwd_f64, 36)
+TM2(jwv_m_wpt2d_rev_f64, 37)
+int jwv_m_modwt_fwd_batch_f64(const double* x, double* wv, int64_t b, int64_t n, int J,
+                              const jwv_taps* t, jwv_mctx* m) {
+  return rec("jwv_m_modwt_fwd_batch_f64", x, b * n, wv, b * (J + 1) * n, 38, t, b, n, J, m->n, 0,
+             0);
+}
+int jwv_m_modwt_inv_batch_f64(const double* wv, double* x, int64_t b, int64_t n, int J,
+                              const jwv_taps* t, jwv_mctx* m) {
+  return rec("jwv_m_modwt_inv_batch_f64", wv, b * (J + 1) * n, x, b * n, 39, t, b, n, J, m->n, 0,
+             0);
+}
+int jwv_modwt_fwd_batch_f64(const double* x, double* wv, int64_t b, int64_t n, int J,
+                            const jwv_taps* t, jwv_ctx* c) {
+  return rec("jwv_modwt_fwd_batch_f64", x, b * n, wv, b * (J + 1) * n, 40, t, b, n, J, 0, 0, 0);
+}
+int jwv_modwt_inv_batch_f64(const double* wv, double* x, int64_t b, int64_t n, int J,
+                            const jwv_taps* t, jwv_ctx* c) {
+  return rec("jwv_modwt_inv_batch_f64", wv, b * (J + 1) * n, x, b * n, 41, t, b, n, J, 0, 0, 0);
+}

@@ -85,9 +85,15 @@ def _declare(lib):
     lib.Java_jwave_amd_HipNative_mctxLastError.restype = P
     lib.Java_jwave_amd_HipNative_transformBatchMulti.argtypes = ([P, P, J, I, B, P, P, I, I, I]
                                                                  + taps)
+    lib.Java_jwave_amd_HipNative_transform2dMulti.argtypes = ([P, P, J, I, B, P, P, I, I, I, I]
+                                                              + taps)
+    mtaps = [I, I, P, P, P, P]
+    lib.Java_jwave_amd_HipNative_modwtBatchMulti.argtypes = [P, P, J, B, P, P, I, I, I] + mtaps
+    lib.Java_jwave_amd_HipNative_modwtBatch.argtypes = [P, P, J, B, P, P, I, I, I] + mtaps
     for f in ("transform1d", "transformBatch", "transform2d", "transform3d", "transform3dPt",
               "modwt", "aed",
-              "decompose", "ctxCreate", "mctxCreate", "transformBatchMulti"):
+              "decompose", "ctxCreate", "mctxCreate", "transformBatchMulti",
+              "transform2dMulti", "modwtBatchMulti", "modwtBatch"):
         getattr(lib, "Java_jwave_amd_HipNative_" + f).restype = I
     return lib
 
@@ -341,6 +347,57 @@ def test_multi_device_batch_marshaling(jvm):
     assert not jvm.read(jy, x.size).any()
     msg = jvm.native("mctxLastError", m)
     assert jvm.lib.fj_string(msg) == b"fake multi error text"
+    jvm.lib.fj_free(jd)
+    jvm.lib.fj_free(h)
+
+
+def test_multi_device_2d_and_modwt_marshaling(jvm):
+    """HipNative.run2d / modwtForwardBatch under -Djwave.hip.devices
+    (HipParallelTransform 2-D, HipMODWTTransform.forwardMODWT(double[][], J)):
+    transform2dMulti passes the matrix geometry and levels to
+    jwv_m_{fwt,wpt}2d_*, modwtBatchMulti / modwtBatch the batch, length and
+    level to the MODWT batch entries, with (J+1)-row coefficient blocks; a
+    failing status leaves the output untouched."""
+    devs = (ctypes.c_int32 * 2)(0, 1)
+    jd = jvm.lib.fj_iarray(2, ctypes.cast(devs, P))
+    h = jvm.lib.fj_larray(1)
+    assert jvm.native("mctxCreate", jd, h) == 0
+    m = ctypes.cast(jvm.lib.fj_data(h), ctypes.POINTER(ctypes.c_int64))[0]
+    w = _w("Daubechies8")
+    x = np.arange(64 * 32, dtype=np.float64)
+    for kind, fwd, name, k in [(0, 1, b"jwv_m_fwt2d_fwd_f64", 34), (0, 0, b"jwv_m_fwt2d_rev_f64", 35),
+                               (1, 1, b"jwv_m_wpt2d_fwd_f64", 36), (1, 0, b"jwv_m_wpt2d_rev_f64", 37)]:
+        jx, jy = jvm.darray(x), jvm.empty(x.size)
+        assert jvm.native("transform2dMulti", m, kind, fwd, jx, jy, 64, 32, 6, 5,
+                          *jvm.taps(w)) == 0
+        c = jvm.last()
+        assert c.name == name and list(c.a[:5]) == [64, 32, 6, 5, 2]
+        assert np.array_equal(jvm.read(jy, x.size), 2 * x + k)
+    # MODWT batches: 3 signals of 100, J = 4 -> 3 x 5 x 100 coefficients
+    wd = _w("Daubechies4")
+    tap = jvm.taps(wd)
+    mtap = tap[:2] + tap[3:]  # the MODWT natives take no reverse scale
+    xs = np.arange(300, dtype=np.float64)
+    cw = jvm.empty(1500)
+    assert jvm.native("modwtBatchMulti", m, 1, jvm.darray(xs), cw, 3, 100, 4, *mtap) == 0
+    c = jvm.last()
+    assert c.name == b"jwv_m_modwt_fwd_batch_f64" and list(c.a[:4]) == [3, 100, 4, 2]
+    assert c.nin == 300 and c.nout == 1500
+    coef = np.arange(1500, dtype=np.float64)
+    jx = jvm.empty(300)
+    assert jvm.native("modwtBatchMulti", m, 0, jx, jvm.darray(coef), 3, 100, 4, *mtap) == 0
+    c = jvm.last()
+    assert c.name == b"jwv_m_modwt_inv_batch_f64" and c.nin == 1500 and c.nout == 300
+    assert np.array_equal(jvm.read(jx, 300), 2 * coef[:300] + 39)
+    ctx = _ctx(jvm)
+    assert jvm.native("modwtBatch", ctx, 1, jvm.darray(xs), jvm.empty(1500), 3, 100, 4, *mtap) == 0
+    assert jvm.last().name == b"jwv_modwt_fwd_batch_f64"
+    jvm.lib.fc_set_rc(2)
+    jy = jvm.empty(x.size)
+    assert jvm.native("transform2dMulti", m, 0, 1, jvm.darray(x), jy, 64, 32, 6, 5,
+                      *jvm.taps(w)) == 2
+    jvm.lib.fc_set_rc(0)
+    assert not jvm.read(jy, x.size).any()
     jvm.lib.fj_free(jd)
     jvm.lib.fj_free(h)
 

@@ -62,3 +62,64 @@ def test_multi_context_batches(devices):
             m.batch(np.ones((4, 48)), w, 2, True, "wpt")
     finally:
         m.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0], [0, 0, 0, 0]])
+def test_multi_context_2d(devices):
+    """ParallelTransform.forward / reverse(double[][]) over the listed devices
+    (jwv_m_fwt2d_* / jwv_m_wpt2d_*, ParallelTransform.java:70-126): row
+    blocks, one device-to-device exchange (hipMemcpyPeerAsync), column slabs,
+    row-strided staging of the host matrix.  Bit-exact against the oracle at
+    2048^2 and 8192^2 (config 3), forward and reverse; [0, 0, 0] runs on 2
+    (the largest power of two <= 3), and the 4-column matrix on 4 devices
+    runs on 2 (chunks of at least 2 columns).  One physical GPU
+    listed several times: the exchange, threads and staging run for real;
+    distinct physical devices are not available on this pool."""
+    import oracle
+    m = jw.MultiContext(devices)
+    try:
+        for kind, wname, rows, cols, lm, ln in (
+                ("fwt", "Daubechies8", 2048, 2048, 11, 11), ("fwt", "Daubechies8", 8192, 8192, 13, 13),
+                ("fwt", "Haar1", 64, 4, 6, 2), ("fwt", "Daubechies4", 16, 4096, 4, 12),
+                ("wpt", "Symlet8", 1024, 512, 5, 4), ("fwt", "Coiflet1", 256, 128, 0, 3)):
+            w = jw.by_class(wname)
+            x = oracle.java_random_doubles(123456789, rows * cols).reshape(rows, cols)
+            ref = oracle.transform_2d_par(kind, True, w, x, lm, ln, 8)
+            y = m.transform_2d(x, w, lm, ln, True, kind)
+            assert np.array_equal(y, ref), "%s %s fwd %dx%d" % (devices, kind, rows, cols)
+            xr = m.transform_2d(ref, w, lm, ln, False, kind)
+            assert np.array_equal(xr, oracle.transform_2d_par(kind, False, w, ref, lm, ln, 8)), \
+                "%s %s rev %dx%d" % (devices, kind, rows, cols)
+        w = jw.by_class("Daubechies4")
+        with pytest.raises(jw.JWaveFailure, match="given level"):
+            m.transform_2d(np.ones((64, 64)), w, 7, 3)
+    finally:
+        m.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", [[0], [0, 0, 0]])
+def test_multi_context_modwt_batches(devices):
+    """forwardMODWT / inverseMODWT of a batch of signals, contiguous blocks
+    per device (jwv_m_modwt_*_batch_f64): each signal's coefficients equal
+    the oracle's (MODWTTransform.java:256-375), non-power-of-two lengths and
+    the deep levels included."""
+    import oracle
+    w = jw.by_class("Daubechies4")
+    m = jw.MultiContext(devices)
+    try:
+        for b, n, J in ((5, 10000, 8), (3, 1000003, 8), (2, 20000, 13), (4, 37, 5)):
+            x = np.stack([oracle.java_random_doubles(b + i, n) for i in range(b)])
+            c = m.modwt_forward(x, w, J)
+            for i in range(b):
+                assert np.array_equal(c[i], oracle.modwt_forward(w, x[i], J)), \
+                    "%s fwd b=%d n=%d J=%d #%d" % (devices, b, n, J, i)
+            xr = m.modwt_inverse(c, w)
+            for i in range(b):
+                assert np.array_equal(xr[i], oracle.modwt_inverse(w, c[i])), \
+                    "%s inv n=%d J=%d #%d" % (devices, n, J, i)
+        with pytest.raises(ValueError, match="exceeds theoretical limit"):
+            m.modwt_forward(np.ones((2, 100)), w, 7)
+    finally:
+        m.close()
