@@ -100,9 +100,6 @@ struct Fwd1Level {
         } else {
           *reinterpret_cast<double2*>(out + p) = make_double2(a0, a1);
         }
-#ifdef JWV_EXP_NOSTORE_DEEP  // diagnostic builds only
-        if (l == 1)
-#endif
         if (2 * r * NT < own && (2 * (r + 1) * NT <= own || p < own))
           st2_pol(yd, p, d0, d1, sp);
       }

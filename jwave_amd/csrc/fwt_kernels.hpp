@@ -680,10 +680,6 @@ __device__ __forceinline__ void fwt_rev_res_blk(const double* __restrict__ s, Ax
   int h = h0, lev = 0;
   if ((h >> 1) * C <= 64 && nlev > 0) {  // small levels: wave 0 only
     if (tid < 64) {
-#ifdef JWV_REPEAT_SMALL
-     for (int rep2 = 0; rep2 < JWV_REPEAT_SMALL; ++rep2) {
-      JWV_STAMP(44 + rep2);
-#endif
       int hh = h;
       for (int lv = 0; lv < nlev && (hh >> 1) * C <= 64; ++lv, hh <<= 1) {
         JWV_STAMP(16 + lv);
@@ -700,9 +696,6 @@ __device__ __forceinline__ void fwt_rev_res_blk(const double* __restrict__ s, Ax
         }
         wave_lds_sync();
       }
-#ifdef JWV_REPEAT_SMALL
-     }
-#endif
     }
     while (lev < nlev && (h >> 1) * C <= 64) { ++lev; h <<= 1; }
     lds_barrier();

@@ -30,24 +30,9 @@ namespace jwv {
 #define JWV_MOD1_FENCE 2
 #endif
 
-// Diagnostic builds only (tools/diag/diag_modwt.hip; wrong results by design,
-// never defined for the library): JWV_EXP_MOD_NOBAR drops the level barriers,
-// JWV_EXP_MOD_NOWF the inverse's W fetches, JWV_EXP_MOD_NOFP the FP64 sums
-// (the LDS reads stay, combined by an integer xor).
-#ifdef JWV_EXP_MOD_NOBAR
-#define JWV_MOD_BAR() ((void)0)
-#else
-#define JWV_MOD_BAR() lds_barrier()
-#endif
 template <bool FMA>
 __device__ __forceinline__ double mod_mac(double acc, double a, double b) {
-#ifdef JWV_EXP_MOD_NOFP
-  (void)b;
-  return __builtin_bit_cast(double, __builtin_bit_cast(unsigned long long, acc) ^
-                                        __builtin_bit_cast(unsigned long long, a));
-#else
   return mac<FMA>(acc, a, b);
-#endif
 }
 
 // Buffer-resource access for tiles that do not wrap: the block-uniform base
@@ -240,14 +225,14 @@ struct ModFwd1Level {
         if ((r + 1) % JWV_MOD1_FENCE == 0)
           asm volatile("" : "+v"(vv[r].x), "+v"(vv[r].y) :: "memory");
     }
-    JWV_MOD_BAR();
+    lds_barrier();
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int k = tid + r * NT;
       if ((r + 1) * NT <= NP || k < NP)
         *reinterpret_cast<double2*>(lds + kPad + e0 + 2 * k) = vv[r];
     }
-    JWV_MOD_BAR();
+    lds_barrier();
     if constexpr (j < J1)
       ModFwd1Level<L, NT, T, J0, J1, FMA, j + 1, P2, M, SLOW>::run(tp, lds, wout, ldw, t0, N, nf);
   }
@@ -277,7 +262,7 @@ __device__ __forceinline__ void modwt_fwd_tile1_body(const double* __restrict__ 
   else
     load_window<1, NT, MAXP>(lds + pad, src, G::W, false, 0, 1,
                              [&](int e) { return wrap_mod(t0 - G::S + e, N); });
-  JWV_MOD_BAR();
+  lds_barrier();
   ModFwd1Level<L, NT, T, J0, J1, FMA, J0, P2, M, SLOW>::run(tp, lds, wout, ldw, t0, N, nf);
   const int tid = threadIdx.x;
 #pragma unroll
@@ -359,11 +344,6 @@ struct ModInv1Level {
     constexpr int Wn = T + G::Rin(j);
     const double* row = coef + (int64_t)(j - 1) * ldw;
     const int tid = opaque_tid();
-#ifdef JWV_EXP_MOD_NOWF
-#pragma unroll
-    for (int r = 0; r < MAXP; ++r) pw[r] = (double)(r + tid);
-    return;
-#endif
     if (inside) {
       // buffer loads: block-uniform base in SGPRs, one lane offset, the slot
       // offsets r*NT*8 as scalar offsets (no per-load 64-bit address VALU)
@@ -417,7 +397,7 @@ struct ModInv1Level {
       const int q = tid + r * NT;
       if (r * NT < Wn && ((r + 1) * NT <= Wn || q < Wn)) wb[q] = pw[r];
     }
-    JWV_MOD_BAR();
+    lds_barrier();
     if constexpr (j > J0) Next::fetch(pw, coef, ldw, t0, N, inside);
     Nf nf{f, bad};
     if constexpr (SLOW && j >= 2)
@@ -522,7 +502,7 @@ struct ModInv1Level {
         if ((r + 1) % JWV_MOD1_FENCE == 0)
           asm volatile("" : "+v"(vv[r].x), "+v"(vv[r].y) :: "memory");
     }
-    JWV_MOD_BAR();
+    lds_barrier();
     if constexpr (j == J0) {
       const bool dfast = t0 + T <= N && (((uintptr_t)(dst + t0)) & 15) == 0;
 #pragma unroll
@@ -641,7 +621,7 @@ struct ModInv1Level {
       }
       asm volatile("" ::: "memory");  // slot fence
     }
-    JWV_MOD_BAR();
+    lds_barrier();
     // final level, whole tile inside the signal, 16-B aligned output: buffer stores
     const bool dfast = j == J0 && t0 + T <= N && (((uintptr_t)(dst + t0)) & 15) == 0;
 #pragma unroll
