@@ -2,6 +2,7 @@
 // (fwt8_kernels.hpp) for one math mode (compiled twice).
 #include "fwt16_kernels.hpp"
 #include "fwt1_row.hpp"
+#include "fwt_colres.hpp"
 #include "jwv_launch.hpp"
 
 #ifndef JWV_FMA
@@ -117,6 +118,21 @@ hipError_t res16_cw(const Bank& b, const ResArgs& a, hipStream_t s) {
                      a.inner, tp);
   return hipGetLastError();
 }
+// forward column tails with compile-time geometry (fwt_colres.hpp); r06 A/B
+// (profiles/r06/ab_col_tail_cres.txt): config 3 forward column tail 51.7 us
+// (fwt_fwd_res) -> 46.7 (256 threads) / 45.5 us (512 threads)
+constexpr int kCresH = 1024, kCresNT = 512;
+template <int L>
+hipError_t cres8_l(const Bank& b, const ResArgs& a, hipStream_t s) {
+  auto k = fwt_fwd_cres8<L, kCresNT, kCresH, kFMA>;
+  const size_t lds = (size_t)kCresH * kCresP * sizeof(double);
+  if (hipError_t e = prep1(k, lds)) return e;
+  FwdTaps<L> tp;
+  for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
+  const dim3 grid((unsigned)(a.nouter * (a.inner / 8)));
+  JWV_LAUNCH(k, grid, dim3(kCresNT), lds, s, a.src, a.sv, a.dst, a.dv, a.nlev, a.inner, tp);
+  return hipGetLastError();
+}
 template <int L>
 hipError_t res16_l(const Bank& b, const ResArgs& a, hipStream_t s, bool fwd) {
   // the half-slab pairing is a bijection for whole groups of 16 blocks
@@ -129,10 +145,22 @@ namespace JWV_NS {
 // Reverse resident tails of column passes with one wave per column
 // (fwt1_row.hpp): XCD-paired half slabs, 16-B aligned row segments, a
 // compiled-in tap count, at most kSmallH rows.  Config 3 reverse column tail
-// 74-75 -> 60-61 us (r04h: 16-column blocks 69 us); the forward keeps the
-// block-per-slab kernel (70 us against 73 / 90 us for 16 / 8 columns).
+// 74-75 -> 60-61 us (r04h: 16-column blocks 69 us).  Forward tails of 1024
+// rows take the compile-time block-per-slab kernel (fwt_colres.hpp); other
+// forward heights fall back to the generic fwt_fwd_res.
 bool fwt_res16(const Bank& b, const ResArgs& a, hipStream_t s, bool fwd, hipError_t& err) {
-  if (fwd) return false;
+  if (fwd) {
+    // forward column tails of 1024 rows, 8-column slabs (config 3)
+    if (!a.dma || a.inner % 8 || a.n != kCresH || a.nlev < 1 || a.nlev > 10 ||
+        a.sv.pk != 1 || a.dv.pk != 1 || (a.sv.s_len & 1) || (a.dv.s_len & 1) ||
+        (a.sv.s_outer & 1) || (a.dv.s_outer & 1) || (((uintptr_t)a.src | (uintptr_t)a.dst) & 15))
+      return false;
+    switch (b.L) {
+      case 8: err = cres8_l<8>(b, a, s); return true;
+      case 16: err = cres8_l<16>(b, a, s); return true;
+      default: return false;
+    }
+  }
   if (!a.dma || a.inner % kColW || a.nlev < 1 || a.sv.pk != 1 || a.dv.pk != 1) return false;
   if (!fwd && b.scale != 1.0) return false;
   if ((a.sv.s_len & 1) || (a.dv.s_len & 1) || (a.sv.s_outer & 1) || (a.dv.s_outer & 1) ||

@@ -497,6 +497,24 @@ def test_3d_long_lines(ctx, wname):
                      oracle.transform_3d("fwt", False, w, yr, lp, lq, lr), "3d rev")
 
 
+@pytest.mark.parametrize("wname", ["Daubechies4", "Daubechies8", "Symlet8", "Coiflet1"])
+def test_fwt2d_column_tail(ctx, ctx_fma, wname):
+    """The forward column pass's resident tail over 1024 rows (fwt_colres.hpp,
+    compile-time geometry, 8-column slabs, padded conflict-free rows) at every
+    level count: matrices of 1024 rows (the tail from level 0) and 8192 rows
+    (after the tile pass), slab counts that are and are not whole XCD pairs."""
+    w = jw.by_class(wname)
+    for r, c in ((1024, 64), (1024, 256), (8192, 32)):
+        x = rnd(r * c, r + c).reshape(r, c)
+        for lm in range(1, r.bit_length()):
+            ln = 3
+            yr = oracle.transform_2d("fwt", True, w, x, lm, ln)
+            assert_exact(T.transform_2d(x, w, lm, ln, True, ctx), yr,
+                         "%s col tail %dx%d lm=%d" % (wname, r, c, lm))
+            assert_close(T.transform_2d(x, w, lm, ln, True, ctx_fma), yr,
+                         "%s col tail fma %dx%d lm=%d" % (wname, r, c, lm))
+
+
 def test_fwt2d_config3_full_size(ctx, ctx_fma):
     """Config 3 at full size: Daubechies8, 8192 x 8192, levels 13 x 13
     (BasicTransform.java:361-474), both directions bit-exact vs the oracle in
