@@ -155,6 +155,55 @@ __device__ __forceinline__ void fwd_couple_pipe(const FwdTaps<L>& tp, const doub
   d1 = sd1;
 }
 
+// fwd_couple_pipe over three adjacent pairs (x, x + 2, x + 4; six sums): the
+// WPT forward trio tiles (wpt1_kernels.hpp).  Same per-output operations and
+// order as fwd_pair (bit-exact); FMA mode keeps its fused form.
+template <int L, bool FMA, int G, bool ZS = true>
+__device__ __forceinline__ void fwd_trio_pipe(const FwdTaps<L>& tp, const double* x, double* a,
+                                              double* d) {
+  static_assert(L % G == 0, "tap groups");
+  double sa[3] = {0.0, 0.0, 0.0}, sd[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+  for (int j0 = 0; j0 < L; j0 += G) {
+    double pa[3][G], pd[3][G];
+    if constexpr (!FMA) {
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          pa[p][g] = x[j0 + g + 2 * p] * tp.lo[j0 + g];
+          pd[p][g] = x[j0 + g + 2 * p] * tp.hi[j0 + g];
+        }
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) asm volatile("" : "+v"(pa[p][g]), "+v"(pd[p][g]));
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        if constexpr (FMA) {
+          sa[p] = __builtin_fma(x[j0 + g + 2 * p], tp.lo[j0 + g], sa[p]);
+          sd[p] = __builtin_fma(x[j0 + g + 2 * p], tp.hi[j0 + g], sd[p]);
+        } else if (!ZS && j0 == 0 && g == 0) {
+          sa[p] = pa[p][0];
+          sd[p] = pd[p][0];
+        } else {
+          sa[p] = sa[p] + pa[p][g];
+          sd[p] = sd[p] + pd[p][g];
+        }
+      }
+#pragma unroll
+    for (int p = 0; p < 3; ++p) asm volatile("" : "+v"(sa[p]), "+v"(sd[p]));
+  }
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+    a[p] = sa[p];
+    d[p] = sd[p];
+  }
+}
+
 // A reverse couple (pairs m, m+1; A/D point at a[m], d[m]) with the products
 // of G terms issued ahead of their adds:
 // per group 8G independent multiplies (a*lor, d*hir of both pairs, even and

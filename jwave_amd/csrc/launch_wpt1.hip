@@ -53,13 +53,14 @@ hipError_t wrev1_k(const Bank& b, const TileArgs& a, hipStream_t s) {
 // 8192-sample forward WPT tiles, 512 threads: half the halo recompute of the
 // 4096 tile (14.7% -> 7.4% extra pairs) at the same waves per CU.  Config 4
 // forward 2597 -> 2468 us; the reverse (halo ~7% at 4096) measured no gain
-// and keeps 4096.
+// and keeps 4096.  Levels in trio form (wpt_fwd_tile3, r06: EXACT forward
+// -0.7%, FMA forward -4.3%, profiles/r06/ab_trio_wpt_fwt.txt).
 template <int L>
 hipError_t wpt8k_fwd(const Bank& b, const TileArgs& a, hipStream_t s) {
   constexpr int TT = 8192, K = 6;
   const dim3 grid((unsigned)(a.nouter * (a.h / TT)));
-  auto k = wpt_fwd_tile1<L, 512, TT, K, kFMA>;
-  const size_t lds = (size_t)Wpt1FwdGeo<L, TT, K>::lds_doubles() * sizeof(double);
+  auto k = wpt_fwd_tile3<L, 512, TT, K, kFMA>;
+  const size_t lds = (size_t)Wpt3FwdGeo<L, TT, K>::lds_doubles() * sizeof(double);
   if (hipError_t e = prep1(k, lds)) return e;
   FwdTaps<L> tp;
   for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }

@@ -105,6 +105,126 @@ struct Wpt1FwdLevel {
   }
 };
 
+// Trio form of the forward tile: a lane computes three adjacent pairs
+// (3k .. 3k+2 of a sub-window) from L + 4 samples.  Couples start 4 doubles
+// (two 16-B units) apart, so the 16 lanes of a ds_read_b128 group land on 8
+// of the 16 unit slots of a bank row (2-way conflicts on every window read,
+// SQ r06: 41.6% of LDS-active cycles); trios start 3 units apart and 3 is
+// odd, so the group covers all 16 slots.  A trio also reads 10 units for 6
+// outputs instead of 9 for 4 and spreads the per-slot address work over 6.
+// Sub-windows are padded to whole trios (stride st(l), even): the trio that
+// runs past a sub-window's last pair reads the next window's start (or the
+// tail pad) and writes its surplus pairs into the padding, so only the level
+// that stores to HBM needs a per-pair predicate.
+template <int L, int T, int K>
+struct Wpt3FwdGeo {
+  static constexpr int m(int l) { return Wpt1FwdGeo<L, T, K>::m(l); }
+  static constexpr int trios(int l) { return (m(l) + 2) / 3; }  // per sub-window of level l
+  static constexpr int st(int l) { return l == 0 ? m(0) : (3 * trios(l) + 1) & ~1; }
+  static constexpr int lds_doubles() {
+    int n = m(0);
+    for (int l = 1; l <= K; ++l) {
+      const int rd = ((1 << (l - 1)) - 1) * st(l - 1) + 6 * (trios(l) - 1) + L + 4;
+      n = rd > n ? rd : n;
+      const int wr = l < K ? (1 << l) * st(l) : 0;
+      n = wr > n ? wr : n;
+    }
+    return (n + 1) & ~1;
+  }
+};
+
+template <int L, int NT, int T, int K, bool FMA, int l>
+struct Wpt3FwdLevel {
+  // lds: 2^(l-1) input sub-windows (stride st(l-1)); writes 2^l sub-windows
+  // of m(l) samples at stride st(l) (a: 2s, d: 2s + 1)
+  __device__ __forceinline__ static void run(const FwdTaps<L>& tp, double* lds, int h, int t,
+                                             double* __restrict__ y) {
+    using G = Wpt3FwdGeo<L, T, K>;
+    constexpr int mi = G::st(l - 1), mo = G::m(l), so = G::st(l), M = G::trios(l);
+    constexpr int NC = (1 << (l - 1)) * M;
+    constexpr int R = (NC + NT - 1) / NT;
+    const int tid = opaque_tid();
+    double ra[R][3], rd[R][3];
+    int wo[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int q = tid + r * NT;
+      if ((r + 1) * NT <= NC || q < NC) {
+        const int s = (int)((unsigned)q / (unsigned)M);  // sub-window
+        const int k = q - s * M;                          // trio
+        wo[r] = (2 * s) * so + 3 * k;
+        const double* in = lds + s * mi + 6 * k;
+        double x[L + 4];
+#pragma unroll
+        for (int j = 0; j < L + 4; j += 2) {
+          const double2 v = *reinterpret_cast<const double2*>(in + j);
+          x[j] = v.x;
+          x[j + 1] = v.y;
+        }
+        double a[3], d[3];
+        fwd_trio_pipe<L, FMA, 2, l == K>(tp, x, a, d);
+        asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(d[0]), "+v"(d[1]),
+                     "+v"(d[2]) :: "memory");  // slot boundary
+        if constexpr (l == K) {
+          // packets 2s (a) and 2s+1 (d) of size h/2^K; own range t*T/2^K + 3k
+          const int hp = h >> K;
+          double* pa = y + (int64_t)(2 * s) * hp + t * (T >> K) + 3 * k;
+          double* pd = pa + hp;
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            if (mo % 3 == 0 || 3 * k + p < mo) {
+              pa[p] = a[p];
+              pd[p] = d[p];
+            }
+        } else {
+#pragma unroll
+          for (int p = 0; p < 3; ++p) {
+            ra[r][p] = a[p];
+            rd[r][p] = d[p];
+          }
+        }
+      }
+    }
+    if constexpr (l < K) {
+      lds_barrier();
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int q = tid + r * NT;
+        if ((r + 1) * NT <= NC || q < NC) {
+#pragma unroll
+          for (int p = 0; p < 3; ++p) {
+            lds[wo[r] + p] = ra[r][p];
+            lds[wo[r] + so + p] = rd[r][p];
+          }
+        }
+      }
+      lds_barrier();
+      Wpt3FwdLevel<L, NT, T, K, FMA, l + 1>::run(tp, lds, h, t, y);
+    }
+  }
+};
+
+// Grid and window as wpt_fwd_tile1; the levels in trio form.
+template <int L, int NT, int T, int K, bool FMA>
+__global__ __launch_bounds__(NT) void wpt_fwd_tile3(const double* __restrict__ src, AxisView sv,
+                                                    double* __restrict__ dst, AxisView dv, int h,
+                                                    FwdTaps<L> tp) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  constexpr int M0 = Wpt3FwdGeo<L, T, K>::m(0);
+  const int ntile = h / T;
+  const int nblk = gridDim.x;
+  int b = blockIdx.x;
+  if ((nblk & 7) == 0) b = (b & 7) * (nblk >> 3) + (b >> 3);
+  const int t = b % ntile;
+  const int64_t o = b / ntile;
+  const double* s = src + view_base(sv, o);
+  const int msk = h - 1, base = t * T;
+  load_window<1, NT, (M0 + NT - 1) / NT>(lds, s, M0, true, 0, 1,
+                                          [&](int e) { return (int64_t)((base + e) & msk); });
+  dma_fence_barrier();
+  Wpt3FwdLevel<L, NT, T, K, FMA, 1>::run(tp, lds, h, t, dst + view_base(dv, o));
+}
+
 // Grid: rows * (h / T) blocks; row o = packet o of the pass input (view sv,
 // packets addressed through view_base); output rows likewise (view dv).
 template <int L, int NT, int T, int K, bool FMA>
