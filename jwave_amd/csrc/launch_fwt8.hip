@@ -57,17 +57,21 @@ hipError_t rev8_k(const Bank& b, const TileArgs& a, hipStream_t s) {
 // Forward 512-row tiles (78 KB of LDS at L = 16: 2 blocks per CU), reverse
 // 256-row tiles (every window in LDS: 61 KB).  Config 3 against the C = 8
 // tiles (r04b, one box, two rounds): 1.368 / 1.371 -> 1.341 / 1.334 ms/step.
-constexpr int kT16F = 512, kT16R = 256;
+// r06 (profiles/r06/ab_col16_geometry.txt): forward blocks of 512 threads
+// (4 waves per SIMD at 2 blocks per CU) -8.8 us per column pass against 256;
+// 256-row tiles (3 blocks per CU, 38% halo) and 1024-row tiles (1 block of
+// 1024 threads) slower.
+constexpr int kT16F = 512, kT16R = 256, kNT16F = 512;
 constexpr bool kRev16IP = true;  // Rev1Geo in-place layout: 61 -> 39 KB, 2 -> 4 blocks per CU
 template <int L, int K>
 hipError_t fwd16_k(const Bank& b, const TileArgs& a, hipStream_t s) {
-  auto k = fwt_fwd_tile16<L, 256, kT16F, K, kFMA>;
+  auto k = fwt_fwd_tile16<L, kNT16F, kT16F, K, kFMA>;
   const size_t lds = (size_t)Fwd16Geo<L, kT16F, K>::lds_doubles() * sizeof(double);
   if (hipError_t e = prep1(k, lds)) return e;
   FwdTaps<L> tp;
   for (int j = 0; j < L; ++j) { tp.lo[j] = b.lo[j]; tp.hi[j] = b.hi[j]; }
   const dim3 grid((unsigned)(a.nouter * (a.inner / 16) * (a.h / kT16F)));
-  JWV_LAUNCH(k, grid, dim3(256), lds, s, a.src, a.sv, a.dst, a.dv, a.adst, a.av, a.h,
+  JWV_LAUNCH(k, grid, dim3(kNT16F), lds, s, a.src, a.sv, a.dst, a.dv, a.adst, a.av, a.h,
                      a.inner, tp, Geo::slab_order());
   return hipGetLastError();
 }
