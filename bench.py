@@ -485,12 +485,15 @@ def cpu_baseline(spec, seconds):
 
 
 # --------------------------------------------------------------- roofline
-def load_traffic(workload, kernel, math):
+def load_traffic(workload, kernel, math, lib_sha=None):
     """HBM bytes per launch of `kernel` in `workload` from the committed
-    rocprofv3 PMC summaries (profiles/pmc_*.json, key "workload:kernel/math");
-    None when no summary covers that workload's kernel."""
+    rocprofv3 PMC summaries (profiles/pmc_*.json, key "workload:kernel/math"),
+    preferring a summary taken with the library being measured (its
+    build.lib_sha256, recorded by tools/pmc_traffic.py); (None, None, None)
+    when no summary covers that workload's kernel."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
+    found = []
     for f in reversed(files):
         try:
             d = json.load(open(f))
@@ -498,8 +501,12 @@ def load_traffic(workload, kernel, math):
             continue
         ent = d.get("kernels", {}).get("%s:%s/%s" % (workload, kernel, math))
         if ent and ent.get("hbm_bytes_per_launch"):
-            return float(ent["hbm_bytes_per_launch"]), os.path.relpath(f, ROOT)
-    return None, None
+            found.append((float(ent["hbm_bytes_per_launch"]), os.path.relpath(f, ROOT),
+                          (d.get("build") or {}).get("lib_sha256")))
+    for t in found:
+        if lib_sha and t[2] == lib_sha:
+            return t
+    return found[0] if found else (None, None, None)
 
 
 def timed(d, step, steps, issue=None):
@@ -705,13 +712,17 @@ def measure(args, d, W, workload, steps, warmup, math):
         avg_ms = ks["total_ms"] / ks["launches"]
         bytes_per_launch = ks["bytes"] / ks["launches"]
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-        traffic, tsrc = load_traffic(workload, kname, math)
+        from jwave_amd import _lib as _L
+        lib_sha = _L.provenance().get("lib_sha256")
+        traffic, tsrc, tsha = load_traffic(workload, kname, math, lib_sha)
         r["roof"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                      "kernel": kname, "avg_launch_us": round(avg_ms * 1e3, 2),
                      "algorithmic_bytes_per_launch": bytes_per_launch, "launches": ks["launches"]}
         if tsrc:
             r["roof"]["traffic_source"] = tsrc
+            r["roof"]["traffic_lib_sha256"] = tsha
+            r["roof"]["traffic_same_lib"] = bool(lib_sha) and tsha == lib_sha
         if W.get("flops_per_sample"):
             # second bound: algorithmic FP64 flops of the
             # dominant launch over its time; EXACT mode issues mul and add

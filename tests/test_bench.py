@@ -64,4 +64,18 @@ def test_cpu_baseline_legs(kind):
 def test_load_traffic_is_keyed_by_workload():
     import bench
     # no committed summary holds a "nosuch" workload: never borrow another's bytes
-    assert bench.load_traffic("nosuch", "fwt_fwd_tile", "exact") == (None, None)
+    assert bench.load_traffic("nosuch", "fwt_fwd_tile", "exact") == (None, None, None)
+
+
+def test_load_traffic_prefers_the_measured_library(tmp_path, monkeypatch):
+    import bench
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    key = "fwt2d:fwt_fwd_tile/exact"
+    for name, sha, b in (("pmc_a.json", "aaaa", 1.0), ("pmc_b.json", "bbbb", 2.0)):
+        (prof / name).write_text(json.dumps({"build": {"lib_sha256": sha},
+                                             "kernels": {key: {"hbm_bytes_per_launch": b}}}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    assert bench.load_traffic("fwt2d", "fwt_fwd_tile", "exact", "aaaa") == (1.0, "profiles/pmc_a.json", "aaaa")
+    # no summary of that library: the latest one, with its own digest
+    assert bench.load_traffic("fwt2d", "fwt_fwd_tile", "exact", "cccc") == (2.0, "profiles/pmc_b.json", "bbbb")

@@ -3,8 +3,8 @@
 #   gpu_final.sh TAG a   GPU parity suite + smoke, bench lines for every
 #                        workload (driver-shaped 20/5 for config 2, FMA line),
 #                        rocprofv3 kernel stats per workload
-#   gpu_final.sh TAG b   PMC FETCH/WRITE traffic per workload, SQ counters of
-#                        the MODWT and WPT tiles
+#   gpu_final.sh TAG b   PMC FETCH/WRITE traffic per workload (+ FMA WPT), SQ
+#                        counters of the MODWT, WPT and 2-D FWT kernels
 set -o pipefail
 export JWAVE_AMD_NO_BUILD=1
 TAG=${1:-final}; PART=${2:-a}
@@ -24,8 +24,10 @@ if [ "$PART" = a ]; then
   done
 else
   bash tools/gpu_pmc.sh $TAG/pmc exact fwt1d fwt2d wpt modwt || exit 6
-  for wl in modwt wpt; do
+  bash tools/gpu_pmc.sh $TAG/pmc_fma fma wpt || exit 6
+  for wl in modwt wpt fwt2d; do
     bash tools/gpu_sqpmc_wl.sh $TAG/sq_$wl $wl > $O/sq_$wl.txt 2>&1 || { echo SQ $wl FAILED; tail $O/sq_$wl.txt; exit 7; }
   done
+  bash tools/gpu_sqpmc_wl.sh $TAG/sq_wpt_fma wpt fma > $O/sq_wpt_fma.txt 2>&1 || { echo SQ wpt fma FAILED; tail $O/sq_wpt_fma.txt; exit 7; }
   echo part b done
 fi

@@ -19,6 +19,7 @@ usage: pmc_traffic.py WORKLOAD MATH FETCH_DIR FETCH_LOG WRITE_DIR WRITE_LOG OUT.
 """
 import csv
 import glob
+import hashlib
 import json
 import os
 import sys
@@ -65,6 +66,18 @@ def attribute(dirpath, counter, logfile):
     return per
 
 
+def lib_record():
+    """Digest of the library the counter passes loaded (JWAVE_AMD_LIB or the
+    in-tree build): bench.py's build.lib_sha256 of the same file."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.environ.get("JWAVE_AMD_LIB") or os.path.join(root, "jwave_amd", "lib", "libjwave_hip.so")
+    h = hashlib.sha256()
+    with open(lib, "rb") as fh:
+        for blk in iter(lambda: fh.read(1 << 20), b""):
+            h.update(blk)
+    return {"lib": os.path.relpath(lib, root), "lib_sha256": h.hexdigest()[:16]}
+
+
 def main():
     workload, math, fdir, flog, wdir, wlog, out = sys.argv[1:8]
     fetch = attribute(fdir, "FETCH_SIZE", flog)
@@ -74,7 +87,7 @@ def main():
     w_fac = CALIB_BYTES / (1024.0 * sum(cw["kb"]) / len(cw["kb"])) if cw else 1.0
     res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), "
                      "dispatches attributed by the library's launch log",
-           "workload": workload, "math": math,
+           "workload": workload, "math": math, "build": lib_record(),
            "calibration": {"kernel": "copy_axis", "known_bytes_each_way": CALIB_BYTES,
                            "fetch_factor": f_fac, "write_factor": w_fac,
                            "note": "bytes = counter_KB * 1024 * factor"},
