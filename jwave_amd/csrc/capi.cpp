@@ -109,7 +109,7 @@ void nt_copy(void* dst, const void* src, size_t n) {
   else nt_copy256((char*)dst, (const char*)src, n);
 }
 #else
-void nt_copy(void* dst, const void* src, size_t n);  // host code only
+void nt_copy(void*, const void*, size_t) {}  // the device pass never runs host code
 #endif
 
 // Host threads for the pageable <-> pinned copies (one core's memcpy is
@@ -411,10 +411,10 @@ struct ProfScope {
     jwv::g_launch_ev = {};
     const jwv_ctx::Rec& r = c->recs[idx];
     if (n == 0) {  // nothing launched (a copy): an empty span
-      hipEventRecord(r.e0, c->stream);
-      hipEventRecord(r.e1, c->stream);
+      (void)hipEventRecord(r.e0, c->stream);
+      (void)hipEventRecord(r.e1, c->stream);
     } else if (n > 1) {  // several launches: first start to last end
-      hipEventRecord(r.e1, c->stream);
+      (void)hipEventRecord(r.e1, c->stream);
     }
   }
 };
@@ -1681,21 +1681,21 @@ int jwv_ctx_destroy(jwv_ctx* c) {
   if (!c) return JWV_OK;
   int prev = -1;
   if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-  hipSetDevice(c->device);
-  hipStreamSynchronize(c->stream);
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->ws[0], &c->ws[1], &c->big, &c->big2, &c->red, &c->hin, &c->hout})
-    if (b->p) hipFree(b->p);
-  if (c->sync) hipFree(c->sync);
-  for (auto& r : c->recs) { hipEventDestroy(r.e0); hipEventDestroy(r.e1); }
-  for (auto e : c->ev_pool) hipEventDestroy(e);
-  if (c->switch_ev) hipEventDestroy(c->switch_ev);
+    if (b->p) (void)hipFree(b->p);
+  if (c->sync) (void)hipFree(c->sync);
+  for (auto& r : c->recs) { (void)hipEventDestroy(r.e0); (void)hipEventDestroy(r.e1); }
+  for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+  if (c->switch_ev) (void)hipEventDestroy(c->switch_ev);
   for (int i = 0; i < kPinSlots; ++i) {
-    if (c->pin.p[i]) hipHostFree(c->pin.p[i]);
-    if (c->pin.ev[i]) hipEventDestroy(c->pin.ev[i]);
+    if (c->pin.p[i]) (void)hipHostFree(c->pin.p[i]);
+    if (c->pin.ev[i]) (void)hipEventDestroy(c->pin.ev[i]);
   }
-  if (c->own) hipStreamDestroy(c->own);
+  if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
-  if (prev >= 0) hipSetDevice(prev);
+  if (prev >= 0) (void)hipSetDevice(prev);
   return JWV_OK;
 }
 

@@ -19,7 +19,6 @@ namespace jwv {
 namespace {
 constexpr bool kFMA = JWV_FMA != 0;
 constexpr int NT = 256;
-constexpr int T = Geo::kModT;
 constexpr int TI = Geo::kModTInv;  // inverse: two windows in LDS, smaller tile
 constexpr int SMAX = Geo::kModS;
 

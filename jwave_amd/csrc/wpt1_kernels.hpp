@@ -395,8 +395,9 @@ struct Wpt1RevLevel {
     // head pairs: lane -> (window hs, global pair hm)
     int hs = -1, hml = 0;
     double hxe = 0.0, hxo = 0.0;
-    if (head_tile && tid < NW * (Q - 1)) {
-      const int s = tid / (Q - 1), m = tid % (Q - 1), ml = m - pbase;
+    if (Q > 1 && head_tile && tid < NW * (Q - 1)) {
+      constexpr int Q1 = Q > 1 ? Q - 1 : 1;  // Haar (Q = 1) has no head pairs
+      const int s = tid / Q1, m = tid % Q1, ml = m - pbase;
       if (ml >= 0 && ml < NPW) {
         const double* ab = lds + (2 * s) * li_;
         const double* db = ab + li_;
