@@ -144,4 +144,129 @@ __global__ __launch_bounds__(NT) void fwt_fwd_cres8(const double* __restrict__ s
   }
 }
 
+
+// ------------------------------------------------------------------ reverse
+// Reverse column tail with compile-time geometry (config 3: 8-column slabs,
+// levels of output size 2 .. HTOP = 1024; BasicTransform.reverse(double[][])
+// columns, Wavelet.reverse, Wavelet.java:277-303, through rev_pair /
+// rev_pair_rot_t / rev_small_cH exactly as rev_small_levels takes them:
+// EXACT results are bit-identical to fwt_rev_col16).
+// Rows at a dense pitch of 8 doubles: work item w = (pair m = w >> 3, column
+// c = w & 7), so the 32 lanes of a ds_read_b64 group read 4 consecutive rows
+// = 256 contiguous bytes (conflict-free) at every tap.  Interior pairs
+// (m >= Q-1) read a[m-q], d[m-q] at immediate offsets; the array-head pairs
+// (m < Q-1) all sit in wave 0's first slot, which alone takes the rotated
+// form (rev_small_levels runs the rotated form in slot 0 of every column's
+// wave).  Levels with at most 64 items run on wave 0 with wave-local
+// ordering; a level's outputs overwrite rows [0, hh) after its reads.
+// Element (index i, column c) of the level arrays at lds[i * SI + c * SC]
+// (dense rows of 8 columns: SI = 8, SC = 1).  The same levels over blocks of
+// 8 rows (SI = 1, SC = a padded row pitch) measured no faster than the
+// wave-per-row tail (r06, profiles/r06/ab_rev_tails_ct.txt) and are not built.
+template <int L, int NT, bool FMA, int hh, int HTOP, int SI = 8, int SC = 1>
+struct RevCresLevel {
+  static constexpr int half = hh / 2, Q = L / 2;
+  static constexpr int NI = half * 8;
+  static constexpr bool kWave = NI <= 64;
+  static constexpr int R = kWave ? 1 : (NI + NT - 1) / NT;
+  __device__ __forceinline__ static void run(const RevTaps<L>& tp, const double* tl, double* lds,
+                                             int h0) {
+    if (hh >= h0) {  // block-uniform: the levels below the input size are skipped
+      // the first block-wide level after wave 0's levels: publish them
+      if constexpr (!kWave && hh > 2 && 2 * hh <= 64)
+        if (hh > h0) lds_barrier();
+      const int tid = opaque_tid();
+      if (!kWave || tid < 64) {
+        double xe[R], xo[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int w = tid + r * NT;
+          const int wc = w < NI ? w : NI - 1;
+          const int c = wc & 7, m = wc >> 3;
+          if constexpr (hh < L) {
+            rev_small_cH<L, FMA, hh>(tp, lds + c * SC, lds + half * SI + c * SC, SI, m, xe[r],
+                                     xo[r]);
+          } else {
+            // wave-uniform: does this wave's slot hold array-head pairs?
+            const int mb = (__builtin_amdgcn_readfirstlane(tid & ~63) + r * NT) >> 3;
+            if (mb < Q - 1) {
+              constexpr int hm = half - 1;
+              rev_pair_rot_t<L, FMA>(
+                  tl, [=](int q) { return lds[((m - q) & hm) * SI + c * SC]; },
+                  [=](int q) { return lds[(half + ((m - q) & hm)) * SI + c * SC]; },
+                  m < Q - 1 ? m : Q - 1, xe[r], xo[r]);
+            } else {
+              const double* A = lds + m * SI + c * SC;
+              double av[Q], dv[Q];
+#pragma unroll
+              for (int q = 0; q < Q; ++q) {
+                av[q] = A[-SI * q];
+                dv[q] = A[half * SI - SI * q];
+              }
+              rev_pair<L, FMA>(tp, av, dv, -1, xe[r], xo[r]);
+            }
+          }
+          pin2(xe[r], xo[r]);
+        }
+        if constexpr (kWave) wave_lds_sync(); else lds_barrier();
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int w = tid + r * NT;
+          if ((r + 1) * NT <= NI || w < NI) {
+            const int c = w & 7, m = w >> 3;
+            lds[(2 * m) * SI + c * SC] = xe[r];
+            lds[(2 * m + 1) * SI + c * SC] = xo[r];
+          }
+        }
+      } else if constexpr (!kWave) {
+        lds_barrier();
+      }
+      if constexpr (kWave) {
+        if (tid < 64) wave_lds_sync();
+      } else {
+        lds_barrier();
+      }
+    }
+    if constexpr (hh < HTOP) RevCresLevel<L, NT, FMA, 2 * hh, HTOP, SI, SC>::run(tp, tl, lds, h0);
+  }
+};
+
+// Grid: one block per 8-column slab (res_slab_block pairs the halves of each
+// 128-B line on one XCD).  Rows [0, HTOP) of the slab from src (coefficient
+// prefix), levels of output size h0 .. HTOP, rows [0, HTOP) to dst.  Needs
+// inner % 8 == 0 and 16-B aligned rows (the host checks).
+template <int L, int NT, int HTOP, bool FMA>
+__global__ __launch_bounds__(NT) void fwt_rev_cres8(const double* __restrict__ src, AxisView sv,
+                                                    double* __restrict__ dst, AxisView dv, int h0,
+                                                    int inner, RevTaps<L> tp) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ __attribute__((aligned(16))) double tl[2 * L];
+  stage_rev_taps<L>(tp, tl);
+  const int ncb = inner >> 3;
+  const int64_t bs = res_slab_block<8>(blockIdx.x);
+  const int64_t o = bs / ncb;
+  const int c0 = (int)(bs % ncb) * 8;
+  const double* s = src + view_base(sv, o) + c0;
+  double* y = dst + view_base(dv, o) + c0;
+  {  // rows x 4 16-B units, dense: unit u -> row u >> 2
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int nunits = HTOP * 4;
+    for (int u0 = wave * 64; u0 < nunits; u0 += NT) {
+      const int u = u0 + lane;
+      const double* g = s + (int64_t)(u >> 2) * sv.s_len + 2 * (u & 3);
+      __builtin_amdgcn_global_load_lds((const void*)g,
+                                       (__attribute__((address_space(3))) void*)(lds + 2 * u0),
+                                       16, 0, 0);
+    }
+  }
+  dma_fence_barrier();  // also publishes tl
+  RevCresLevel<L, NT, FMA, 2, HTOP>::run(tp, tl, lds, h0);
+  for (int u = threadIdx.x; u < HTOP * 4; u += NT) {
+    const int r = u >> 2, c = 2 * (u & 3);
+    *reinterpret_cast<double2*>(y + (int64_t)r * dv.s_len + c) =
+        *reinterpret_cast<const double2*>(lds + 8 * r + c);
+  }
+}
+
+
 }  // namespace jwv

@@ -138,6 +138,17 @@ hipError_t cres8_l(const Bank& b, const ResArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 template <int L>
+hipError_t rcres8_l(const Bank& b, const ResArgs& a, hipStream_t s) {
+  auto k = fwt_rev_cres8<L, kCresNT, kCresH, kFMA>;
+  const size_t lds = (size_t)kCresH * 8 * sizeof(double);
+  if (hipError_t e = prep1(k, lds)) return e;
+  RevTaps<L> tp;
+  for (int j = 0; j < L; ++j) { tp.lo_r[j] = b.lo_r[j]; tp.hi_r[j] = b.hi_r[j]; }
+  const dim3 grid((unsigned)(a.nouter * (a.inner / 8)));
+  JWV_LAUNCH(k, grid, dim3(kCresNT), lds, s, a.src, a.sv, a.dst, a.dv, a.n, a.inner, tp);
+  return hipGetLastError();
+}
+template <int L>
 hipError_t res16_l(const Bank& b, const ResArgs& a, hipStream_t s, bool fwd) {
   // the half-slab pairing is a bijection for whole groups of 16 blocks
   const bool half = (a.nouter * (a.inner / 8)) % 16 == 0;
@@ -149,9 +160,11 @@ namespace JWV_NS {
 // Reverse resident tails of column passes with one wave per column
 // (fwt1_row.hpp): XCD-paired half slabs, 16-B aligned row segments, a
 // compiled-in tap count, at most kSmallH rows.  Config 3 reverse column tail
-// 74-75 -> 60-61 us (r04h: 16-column blocks 69 us).  Forward tails of 1024
-// rows take the compile-time block-per-slab kernel (fwt_colres.hpp); other
-// forward heights fall back to the generic fwt_fwd_res.
+// 74-75 -> 60-61 us (r04h: 16-column blocks 69 us).  Tails of 1024 rows take
+// the compile-time block-per-slab kernels (fwt_colres.hpp: forward r06
+// 51.7 -> 45.5 us, reverse -5.8 us against the wave-per-column kernel, which
+// keeps the other heights); other forward heights fall back to the generic
+// fwt_fwd_res.
 bool fwt_res16(const Bank& b, const ResArgs& a, hipStream_t s, bool fwd, hipError_t& err) {
   if (fwd) {
     // forward column tails of 1024 rows, 8-column slabs (config 3)
@@ -163,6 +176,17 @@ bool fwt_res16(const Bank& b, const ResArgs& a, hipStream_t s, bool fwd, hipErro
       case 8: err = cres8_l<8>(b, a, s); return true;
       case 16: err = cres8_l<16>(b, a, s); return true;
       default: return false;
+    }
+  }
+  if (!fwd && a.dma && b.scale == 1.0 && a.inner % 8 == 0 && a.n >= 2 &&
+      a.nlev >= 1 && ((int64_t)a.n << (a.nlev - 1)) == kCresH && a.sv.pk == 1 && a.dv.pk == 1 &&
+      !(a.sv.s_len & 1) && !(a.dv.s_len & 1) && !(a.sv.s_outer & 1) && !(a.dv.s_outer & 1) &&
+      !(((uintptr_t)a.src | (uintptr_t)a.dst) & 15)) {
+    // reverse column tails of 1024 rows, 8-column slabs (config 3)
+    switch (b.L) {
+      case 8: err = rcres8_l<8>(b, a, s); return true;
+      case 16: err = rcres8_l<16>(b, a, s); return true;
+      default: break;
     }
   }
   if (!a.dma || a.inner % kColW || a.nlev < 1 || a.sv.pk != 1 || a.dv.pk != 1) return false;

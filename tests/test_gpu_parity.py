@@ -499,10 +499,11 @@ def test_3d_long_lines(ctx, wname):
 
 @pytest.mark.parametrize("wname", ["Daubechies4", "Daubechies8", "Symlet8", "Coiflet1"])
 def test_fwt2d_column_tail(ctx, ctx_fma, wname):
-    """The forward column pass's resident tail over 1024 rows (fwt_colres.hpp,
-    compile-time geometry, 8-column slabs, padded conflict-free rows) at every
-    level count: matrices of 1024 rows (the tail from level 0) and 8192 rows
-    (after the tile pass), slab counts that are and are not whole XCD pairs."""
+    """The column passes' resident tails over 1024 rows (fwt_colres.hpp,
+    compile-time geometry, 8-column slabs: fwt_fwd_cres8 / fwt_rev_cres8) at
+    every level count, both directions: matrices of 1024 rows (the tails from
+    level 0 / up to the full size) and 8192 rows (beside the tile passes),
+    slab counts that are and are not whole XCD pairs."""
     w = jw.by_class(wname)
     for r, c in ((1024, 64), (1024, 256), (8192, 32)):
         x = rnd(r * c, r + c).reshape(r, c)
@@ -513,6 +514,36 @@ def test_fwt2d_column_tail(ctx, ctx_fma, wname):
                          "%s col tail %dx%d lm=%d" % (wname, r, c, lm))
             assert_close(T.transform_2d(x, w, lm, ln, True, ctx_fma), yr,
                          "%s col tail fma %dx%d lm=%d" % (wname, r, c, lm))
+            xr = oracle.transform_2d("fwt", False, w, yr, lm, ln)
+            assert_exact(T.transform_2d(yr, w, lm, ln, False, ctx), xr,
+                         "%s col tail rev %dx%d lm=%d" % (wname, r, c, lm))
+            assert_close(T.transform_2d(yr, w, lm, ln, False, ctx_fma), xr,
+                         "%s col tail rev fma %dx%d lm=%d" % (wname, r, c, lm))
+
+
+@pytest.mark.parametrize("wname", ["Daubechies4", "Daubechies8", "Coiflet1"])
+def test_fwt2d_row_tail(ctx, ctx_fma, wname):
+    """The row passes' reverse resident tail over 1024-sample row tops
+    (fwt_rev_rres8: 8 rows per block, compile-time levels) at every level
+    count: rows of 1024 (the tail up to the full row) and 8192 samples (under
+    the tile pass); a batch of 72 signals (a partial last block)."""
+    w = jw.by_class(wname)
+    for r, c in ((64, 1024), (64, 8192)):
+        x = rnd(r * c, 7 * r + c).reshape(r, c)
+        for ln in range(1, c.bit_length()):
+            lm = 1 if ln % 3 == 0 else 0
+            yr = oracle.transform_2d("fwt", True, w, x, lm, ln)
+            xr = oracle.transform_2d("fwt", False, w, yr, lm, ln)
+            assert_exact(T.transform_2d(yr, w, lm, ln, False, ctx), xr,
+                         "%s row tail rev %dx%d ln=%d" % (wname, r, c, ln))
+            assert_close(T.transform_2d(yr, w, lm, ln, False, ctx_fma), xr,
+                         "%s row tail rev fma %dx%d ln=%d" % (wname, r, c, ln))
+    # a batch of 72 signals (2-D shapes are powers of two): partial last block
+    x = np.stack([rnd(1024, 300 + i) for i in range(72)])
+    for lev in (1, 4, 10):
+        yr = oracle.batch("fwt", True, w, x, lev)
+        assert_exact(T.fwt_reverse(yr, w, lev, ctx), oracle.batch("fwt", False, w, yr, lev),
+                     "%s row tail rev batch 72 lev=%d" % (wname, lev))
 
 
 def test_fwt2d_config3_full_size(ctx, ctx_fma):
