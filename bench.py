@@ -176,6 +176,39 @@ class PlaceholderBackend:
         x[:n] = c[0, col0:col0 + n]
 
 
+# Algorithmic FP64 flops per sample per direction of each workload (a mul and
+# an add counted apart, as EXACT mode issues them):
+#   fwt1d  Daubechies4, L = 8, full depth: 2L per level-input sample, the
+#          levels' inputs sum to ~2N -> 4L;
+#   fwt2d  Daubechies8, L = 16: the same for the row pass and the column pass;
+#   wpt    Symlet8, L = 16, 6 levels over the whole row each: 6 x 2L;
+#   modwt  Daubechies4, L = 8, J = 8: per level and output L taps on each of
+#          two inputs (forward: V and W outputs; inverse: V and W inputs) -> 4L.
+FLOPS_PER_SAMPLE = {"fwt1d": 4 * 8, "fwt2d": 2 * 4 * 16, "wpt": 6 * 2 * 16, "modwt": 8 * 4 * 8}
+
+
+def step_bounds(workload, math, bytes_per_step, samples_per_step, ms_per_step):
+    """Both floors of one step at one GPU: the algorithmic HBM bytes at the HBM
+    peak and the algorithmic FP64 flops at the FP64 issue ceiling (EXACT: mul
+    and add are separate instructions, so half the FMA-counted peak).  'frac'
+    is the larger floor over the measured step; 'frac_of_sum' the two floors
+    added (a step whose memory and FP64 phases do not overlap at all sits at
+    1.0 of it).  samples_per_step counts both directions, like the line's
+    value."""
+    fps = FLOPS_PER_SAMPLE.get(workload)
+    if fps is None or not ms_per_step:
+        return None
+    flops = fps * samples_per_step
+    ceil = FP64_PEAK_TFLOPS / 2 if math == "exact" else FP64_PEAK_TFLOPS
+    hbm_ms = bytes_per_step / (HBM_PEAK_GBPS * 1e9) * 1e3
+    fp_ms = flops / (ceil * 1e12) * 1e3
+    return {"hbm_floor_ms": round(hbm_ms, 4), "fp64_floor_ms": round(fp_ms, 4),
+            "flops_per_step": flops, "fp64_ceiling_tflops": ceil,
+            "bound": "hbm" if hbm_ms >= fp_ms else "fp64",
+            "frac": round(max(hbm_ms, fp_ms) / ms_per_step, 4),
+            "frac_of_sum": round((hbm_ms + fp_ms) / ms_per_step, 4)}
+
+
 def setup_dry(args, d):
     """--dry-run: a placeholder host step (no transform, no GPU) so the
     launcher, barriers and max-over-ranks timing can be tested on CPU; the
@@ -777,6 +810,8 @@ def secondary_configs(args, d):
                  "roundtrip_max_abs_err": W["check"]()}
             if r["fp64"]:
                 o["roofline_fp64"] = r["fp64"]
+            o["step_bounds"] = step_bounds(wl, math, W["bytes"], W["samples"],
+                                           el / args.steps * 1e3)
             specs[key] = W["cpu"]
             W["ctx"].close()
             del W
@@ -846,6 +881,9 @@ def main():
         out["exchange_ms_per_step"] = round(exch, 4)
     if out_fp64:
         out["roofline_fp64"] = out_fp64
+    if not args.dry_run:
+        out["step_bounds"] = step_bounds(args.workload, args.math, W["bytes"], W["samples"],
+                                         el / args.steps * 1e3)
     if (not args.dry_run and args.workload == "fwt1d" and not args.no_secondary):
         out["batched_wpt_strong"] = secondary_wpt(args, d)
         if d.rank == 0:

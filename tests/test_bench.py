@@ -79,3 +79,22 @@ def test_load_traffic_prefers_the_measured_library(tmp_path, monkeypatch):
     assert bench.load_traffic("fwt2d", "fwt_fwd_tile", "exact", "aaaa") == (1.0, "profiles/pmc_a.json", "aaaa")
     # no summary of that library: the latest one, with its own digest
     assert bench.load_traffic("fwt2d", "fwt_fwd_tile", "exact", "cccc") == (2.0, "profiles/pmc_b.json", "bbbb")
+
+
+def test_step_bounds_floors():
+    """Both floors of a step from the algorithmic counts (DESIGN §6 'Two
+    floors'): config 2 is HBM-bound, config 4 FP64-bound, and FMA math halves
+    the FP64 floor."""
+    import bench
+    n = 1 << 24
+    sb = bench.step_bounds("fwt1d", "exact", 2 * 16.0 * n, 2 * n, 0.1072)
+    assert sb["bound"] == "hbm"
+    assert abs(sb["hbm_floor_ms"] - 2 * 16.0 * n / 8e12 * 1e3) < 1e-4
+    assert abs(sb["fp64_floor_ms"] - 32 * 2 * n / 39.3e12 * 1e3) < 1e-4
+    assert abs(sb["frac"] - sb["hbm_floor_ms"] / 0.1072) < 1e-3
+    b, m = 4096, 1 << 16
+    ex = bench.step_bounds("wpt", "exact", 2 * 16.0 * b * m, 2 * b * m, 4.28)
+    fm = bench.step_bounds("wpt", "fma", 2 * 16.0 * b * m, 2 * b * m, 3.06)
+    assert ex["bound"] == "fp64" and abs(ex["fp64_floor_ms"] - 2.623) < 1e-3
+    assert abs(fm["fp64_floor_ms"] * 2 - ex["fp64_floor_ms"]) < 2e-4
+    assert bench.step_bounds("dry-run", "exact", 1.0, 1, 1.0) is None
